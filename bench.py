@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ray-tracing core on the reference's headline workload.
+
+Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit query
+= the reference's cast_ray calls) and frame ms on world8_stress.json at
+1920x1080, 8 spp, BVH, on N MI355X.
+
+One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
+rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
+the packed RGBA8 rows to rank 0 and the row un-permute.  The frame stays in HBM
+(the PCIe read-back is reported separately as `ms_per_step_with_readback`).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver
+uses torch.distributed.run (one process per GPU, RCCL over xGMI).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch  # first: the HIP runtime torch loads is the one librt_amd.so binds to
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+import rtamd  # noqa: E402
+
+METRIC = "Mrays/sec (primary+secondary) + frame ms, 1080p world8_stress, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
+B_NODE, B_LEAF = 28, 816        # SURVEY §8d algorithmic bytes: BoundingBox / leaf (pose+mesh+12 tris)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--scene", default="world8_stress")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=8)
+    p.add_argument("--brute", action="store_true", help="reference -r: no BVH")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample-rows", type=int, default=2, help="CPU baseline renders rows y %% k == 0")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(args, scene_path):
+    """The reference's CPU path (src/raytracer.cc semantics, restated in oracle/) on a
+    bounded sample of the same workload, 1 thread — the reference's CPU path is serial."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+    orc = Oracle()
+    s = orc.load(scene_path, args.width, args.height)
+    k = max(1, args.cpu_sample_rows)
+    t = time.perf_counter()
+    fr = orc.render(s, semantics=1, use_bvh=0 if args.brute else 1, spp=1, row0=0, row_step=k, nthreads=1, want=())
+    dt = time.perf_counter() - t
+    rays = int(fr["stats"][0])
+    rows = len(range(0, args.height, k))
+    return {
+        "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+        "sample": "%s %dx%d rows y%%%d==0 (%d rows), spp=1, CPU-path semantics of src/raytracer.cc "
+                  "(oracle restatement), 1 thread; %.1f s, %d rays; extrapolated frame at %d spp: %.0f ms"
+                  % (args.scene, args.width, args.height, k, rows, dt, rays, args.spp, dt * k * args.spp * 1e3),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rtamd.set_device(local)
+    scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")
+    scene = rtamd.Scene.load_json(scene_path, args.width, args.height)
+    W, H = scene.width, scene.height
+    rows_per = (H + world - 1) // world                 # padded slice height (equal RCCL message sizes)
+    my_rows = len(range(rank, H, world))
+    part = torch.zeros((rows_per, W), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
+    frame = torch.empty((H, W), dtype=torch.int32, device="cuda") if rank == 0 else None
+    use_bvh = not args.brute
+
+    def step(timing):
+        scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
+                            compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, timing=timing)
+        if world > 1:
+            dist.gather(part, gathered, dst=0)
+            if rank == 0:
+                for r in range(world):                  # un-permute row-cyclic slices
+                    n = len(range(r, H, world))
+                    frame[r::world] = gathered[r][:n]
+        elif rank == 0:
+            frame.copy_(part[:H])
+
+    # per-frame work counters (deterministic): one untimed counted render of this rank's rows
+    st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
+                             compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, sync=True, stats=True)
+    for _ in range(args.warmup):
+        step(False)
+    scene.timing_collect()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    tm = scene.timing_collect()
+    # read-back variant (reference post-condition: framebuffer host readable)
+    t2 = time.perf_counter()
+    host = None
+    for _ in range(max(1, args.steps // 2)):
+        step(False)
+        if rank == 0:
+            host = frame.cpu()
+    torch.cuda.synchronize()
+    rb_ms = (time.perf_counter() - t2) / max(1, args.steps // 2) * 1e3
+
+    local_rays = torch.tensor([st["rays"], st["nodes"], st["leaves"], st["tri_tests"]], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(local_rays, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    rays, nodes, leaves, tris = [float(x) for x in local_rays.cpu()]
+    elapsed = float(tmax.item())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = rays * args.steps / elapsed / 1e6
+    # roofline of the dominant kernel (trace), this rank: algorithmic bytes per launch / event-timed duration
+    trace_ms = tm["trace_ms_total"] / max(1, tm["frames"])
+    bvh_ms = tm["bvh_ms_total"] / max(1, tm["frames"])
+    algo_bytes = B_NODE * st["nodes"] + B_LEAF * st["leaves"] + 4 * W * my_rows
+    achieved = algo_bytes / (trace_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pm = json.load(open(args.pmc))
+            key = "%s_%dx%d_spp%d_n%d" % (args.scene, W, H, args.spp, world)
+            traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "procedural scene from the reference's %s.json (deterministic, no RNG at render time)" % args.scene,
+        "config": {"workload": "%s.json %dx%d %dspp %s" % (args.scene, W, H, args.spp, "brute" if args.brute else "BVH"),
+                   "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bvh": use_bvh,
+                   "parallelism": "row-cyclic x%d + RCCL gather" % world if world > 1 else "single GPU"},
+        "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
+        "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),
+        "tri_tests_per_frame": int(tris), "trace_kernel_ms": round(trace_ms, 4), "bvh_build_ms": round(bvh_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": int(algo_bytes),
+                     "note": "algorithmic bytes = 28*nodes + 816*leaves + 4*W*rows (SURVEY 8d); scene is L2-resident, "
+                             "so frac > 1 is possible"},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, scene_path)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

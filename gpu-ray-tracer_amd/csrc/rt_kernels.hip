@@ -1,0 +1,1080 @@
+// rt_kernels.hip — gfx950 kernels of the ray-tracing core + the C ABI (rt_amd.h).
+//
+// Hot path (BASELINE.json north_star): rtracer::gpu::update_scene
+// (src/raytracer.cu:102-120) = per-frame BVH build + the per-pixel `trace`
+// megakernel running renv::gpu::propagate_ray (src/rayenv/scene.cu:92-188).
+//
+// MI355X design:
+//  * bvh_build: ONE workgroup of 1024 threads builds the whole Morton BVH
+//    (boxes -> 64-bit z-order keys -> LDS bitonic sort of (key, index) == the
+//    reference's stable thrust::sort_by_key -> pairwise level merges), replacing
+//    the reference's 6+ launches and its 1-thread top-level kernel (bvh.cu:64-73).
+//    Nodes are written in heap order (k = 1 .. 2n-1, children 2k / 2k+1) as
+//    32-byte records.
+//  * trace: one lane per pixel, wave = 8x8 pixel tile, block = 16x16.  Each
+//    lane runs the reference's frame-stack integrator as a state machine whose
+//    ONLY wave-collective step is a closest-hit query: every lane with a pending
+//    query (primary, reflection, refraction or shadow segment) traverses the BVH
+//    together.  Traversal is the reference's stackless heap walk made 64-wide:
+//    the node index is wave-uniform (SGPR), node and triangle records are read
+//    with scalar loads, `__ballot` decides descend vs. skip (scene.cu:54-70).
+//    Leaf and box tests use the reference's exact float32 operations, so hit
+//    indices are bit-identical to the single-ray semantics.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rt_math.h"
+#include "rt_scene.h"
+#include "../../include/rt_amd.h"
+
+using namespace rtm;
+using rt::DCamera;
+using rt::DInst;
+using rt::DLight;
+using rt::DMat;
+using rt::DMesh;
+using rt::DNode;
+using rt::DTri;
+
+namespace {
+
+constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
+constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
+constexpr int TRACE_BLOCK = 256;         // 16x16 pixels, 4 waves of 8x8
+
+enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
+enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
+
+__device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b : a; }   // std::max
+// powf of the reference (nvcc pow(float,float)); evaluated in double and rounded:
+// agrees with glibc powf except for 1-ulp cases.
+__device__ __forceinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }
+
+struct Hit {                 // rprimitives::Isect (isect.h:15-24) minus texture data
+    float time;
+    V3 norm;
+    int mat, inst, tri;
+};
+
+struct Counters { unsigned long long rays, nodes, leaves, tris; };
+
+struct SceneView {           // read-only scene data (HBM, L2-resident)
+    const DTri* __restrict__ tris;
+    const DMesh* __restrict__ meshes;
+    const DInst* __restrict__ insts;
+    const DMat* __restrict__ mats;
+    const DLight* __restrict__ lights;
+    const DNode* __restrict__ nodes;
+    int n_leaf, n_inst, n_lights, use_bvh;
+};
+
+// ---------------------------------------------------------------------------
+// Closest hit against one instance: renv::gpu::cast_local (scene.cu:27-40) ->
+// Hitable::hit (hitable.cu:29-38) -> Trimesh::hit_local (trimesh.cu:11-19).
+// `ti` is wave-uniform; the lane's own ray is tested against every triangle of
+// the mesh in index order, accepting t >= 1e-5 && t < h.time (trimesh.cu:56).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool cast_local(const SceneView& S, int ti, const Ray& r, Hit& h, Counters& c) {
+    const DInst inst = S.insts[ti];
+    const DMesh mesh = S.meshes[inst.mesh];
+    c.leaves++;
+    V3 ld = vec_to_local(inst.pose, r.d);
+    float dir_len = len(ld);
+    Ray lr = make_ray(point_to_local(inst.pose, r.o), ld);
+    V3 md = vec_to_local(mesh.pose, lr.d);                  // HitHandle::get_local_ray
+    float scale = len(md);
+    Ray mr = make_ray(point_to_local(mesh.pose, lr.o), md);
+    int best = -1;
+    float bu = 0.0f, bv = 0.0f;
+    const int t0 = mesh.tri_begin, t1 = mesh.tri_begin + mesh.tri_count;
+    c.tris += (unsigned long long)mesh.tri_count;
+    for (int t = t0; t < t1; t++) {
+        const DTri& T = S.tris[t];
+        float time, u, v;
+        if (tri_hit(T.a, T.b, T.c, T.pn, T.area, mr, time, u, v) && time >= THRESH && time < h.time) {
+            h.time = time; best = t; bu = u; bv = v;
+        }
+    }
+    if (best < 0) return false;
+    // interpolated normal of the last accepted triangle (trimesh.cu:58-65)
+    const DTri& T = S.tris[best];
+    float b0 = 1.0f - bu - bv;
+    V3 n = normalized((b0 * T.n0 + bu * T.n1) + bv * T.n2);
+    n = normalized(vec_from_local(mesh.pose, n));            // HitHandle::fix_isect
+    h.time *= scale;
+    h.norm = vec_from_local(inst.pose, n);                   // cast_local
+    h.time *= dir_len;
+    h.mat = T.mat; h.inst = ti; h.tri = best;
+    return true;
+}
+
+// renv::gpu::cast_ray (scene.cu:42-73).  Must be reached by the whole wave with
+// uniform control flow; `active` masks lanes without a pending query.
+__device__ __forceinline__ bool cast_ray(const SceneView& S, bool active, const Ray& r, Hit& h, Counters& c) {
+    bool hit = false;
+    if (active) c.rays++;
+    if (!S.use_bvh || S.n_leaf == 0) {
+        for (int i = 0; i < S.n_inst; i++)
+            if (active && cast_local(S, i, r, h, c)) hit = true;
+        return hit;
+    }
+    const int n = S.n_leaf;
+    if (active) c.nodes++;                                   // root test
+    int k = 1;
+    for (;;) {
+        const DNode nd = S.nodes[k];                          // wave-uniform node -> scalar loads
+        bool hb = active && nd.nd &&
+                  box_hit(v3(nd.mnx, nd.mny, nd.mnz), v3(nd.mxx, nd.mxy, nd.mxz), r);
+        if (k >= n) {                                         // leaf (at_child: 2k >= 2n-1)
+            if (hb && cast_local(S, nd.inst, r, h, c)) hit = true;
+        } else {
+            if (hb) c.nodes += 2;                              // single-ray DFS tests both children
+            if (__ballot(hb)) { k = 2 * k; continue; }          // step_next (bvh.cu:132-140)
+        }
+        while (k & 1) k >>= 1;                                // step_up (bvh.cu:116-130)
+        if (k == 0) break;
+        k += 1;
+    }
+    return hit;
+}
+
+// ---------------------------------------------------------------------------
+// Shading: phong.cu:14-53, light.cu:11-77, scene.cu:14-22
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ V4 phong(const DMat& m, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
+    float nd = max_std(dot(to_light, nrm), 0.0f);
+    V4 diffuse = nd * m.Kd;
+    V3 reflected = reflect(neg(to_light), nrm);
+    float rd = dot(neg(reflected), ray_dir);
+    V4 specular = pow_ref(max_std(rd, 0.0f), m.alpha) * m.Ks;
+    return (diffuse + specular) * incoming;
+}
+
+struct Frame {                // RayFrame (scene.cu:81-90)
+    Ray ray;
+    V3 hit_pt, norm;
+    V4 atten;
+    int last_mat, type, depth, in_obj;
+};
+
+struct TraceParams {
+    DCamera cam;
+    V3 dist_atten;
+    V4 ambience;
+    int W, H, row0, row_step, n_rows, compact, spp, depth;
+    const float2* __restrict__ spp_off;
+    uint32_t* rgba;
+    float4* radiance;
+    int* hit_inst;
+    int* hit_tri;
+    unsigned long long* stats;
+    int* dbg_log;             // debug_cast event log (NULL in normal frames)
+    int dbg_x, dbg_y;
+};
+
+__device__ __forceinline__ void dbg(const TraceParams& P, bool me, int ev) {
+    if (P.dbg_log && me) {
+        int i = atomicAdd(P.dbg_log, 1);
+        if (i < 4094) P.dbg_log[2 + i] = ev;
+    }
+}
+
+// Camera::at (camera.cu:33-42), basis hoisted (bitwise identical, computed on the host)
+__device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
+    float gx = (cx - (0.5f * c.W)) / c.unit;
+    float gy = (0.5f * c.H - cy) / c.unit;
+    V3 dir = (c.near_ * c.f + gx * c.r) + gy * c.u;
+    return make_ray(c.pos, dir);
+}
+
+template <int NF>
+__global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, SceneView S) {
+    // pixel of this lane: 16x16 block tile, 8x8 per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int pr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);    // slice row
+    const bool valid = px < P.W && pr < P.n_rows;
+    const int py = P.row0 + pr * P.row_step;
+    const bool me = valid && px == P.dbg_x && py == P.dbg_y;
+
+    Counters cnt{0, 0, 0, 0};
+    Frame fr[NF];
+    int top = -1, k = 0, phase = valid ? 0 : PH_DONE;
+    bool primary = false;
+    V4 acc = v4(0, 0, 0, 0), sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
+    Hit is{INFINITY, v3(0, 0, 0), 0, -1, -1};                // the pixel's shared Isect
+    int hinst = -1, htri = -1;
+    // illumination state (illuminate / Light::shine / Light::attenuate)
+    int li = 0, fidx = 0;
+    V4 summed = v4(0, 0, 0, 0), rv = v4(0, 0, 0, 0);
+    V3 hpos = v3(0, 0, 0), dtl = v3(0, 0, 0);
+    float da = 1.0f, max_t = 0.0f;
+    Ray q{v3(0, 0, 0), v3(0, 0, 1)};
+
+    // Advance the integrator until the lane needs a query or its pixel is finished.
+    auto advance = [&]() {
+        for (;;) {
+            if (top < 0) {
+                if (phase != 0) {                              // a sample just finished
+                    sum_c = sum_c + v4(acc.x > 1.0f ? 1.0f : acc.x, acc.y > 1.0f ? 1.0f : acc.y,
+                                       acc.z > 1.0f ? 1.0f : acc.z, acc.w > 1.0f ? 1.0f : acc.w);
+                    sum_r = sum_r + acc;
+                    k++;
+                }
+                if (k >= P.spp) { phase = PH_DONE; return; }
+                float2 o = P.spp_off[k];
+                Ray r = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
+                fr[0].ray = r; fr[0].hit_pt = v3(0, 0, 0); fr[0].norm = v3(0, 0, 0);
+                fr[0].atten = v4(1.0f, 1.0f, 1.0f, 1.0f); fr[0].last_mat = -1;
+                fr[0].type = F_NORMAL; fr[0].depth = P.depth; fr[0].in_obj = 0;
+                top = 0; acc = v4(0, 0, 0, 0); primary = (k == 0);
+                is.time = INFINITY;
+            }
+            Frame& f = fr[top];
+            if (f.type == F_NORMAL) {                         // scene.cu:100-128
+                is.time = INFINITY;
+                dbg(P, me, 1);
+                q = f.ray; phase = PH_NORMAL; return;
+            }
+            const DMat& m = S.mats[is.mat];
+            if (f.type == F_REFLECT) {                        // scene.cu:129-148
+                f.type = F_REFRACT;
+                if (m.reflective) {
+                    dbg(P, me, 2);
+                    Frame& c = fr[top + 1];
+                    c.type = F_NORMAL; c.last_mat = f.last_mat; c.in_obj = f.in_obj;
+                    c.atten = f.atten * m.Kr;
+                    c.depth = f.depth - 1;
+                    c.ray = make_ray(f.hit_pt, reflect(f.ray.d, normalized(f.norm)));
+                    top++;
+                }
+                continue;
+            }
+            // F_REFRACT (scene.cu:149-184): reads the possibly clobbered shared Isect
+            if (m.refractive) {
+                dbg(P, me, 3);
+                f.type = F_NORMAL;
+                float n1, n2;
+                if (f.in_obj) { n1 = S.mats[f.last_mat].eta; n2 = 1.0f; }
+                else { n1 = 1.0f; n2 = S.mats[f.last_mat].eta; }
+                bool tir;
+                V3 rd = refract(f.ray.d, normalized(f.norm), n1, n2, tir);
+                if (tir) top--;
+                else { f.ray = make_ray(f.hit_pt, rd); f.in_obj = !f.in_obj; f.depth--; }
+            } else {
+                top--;
+            }
+        }
+    };
+
+    // Issue the shadow query of light `li`, or finish illuminate() when all lights are done.
+    auto next_light = [&]() {
+        if (li < S.n_lights) {
+            const DLight L = S.lights[li];
+            Ray to;
+            if (L.type == 0) {                                 // PointLight::shine (light.cu:63-70)
+                V3 disp = L.v - hpos;
+                float dist = len(disp);
+                float quad = P.dist_atten.x + P.dist_atten.y * dist + P.dist_atten.z * dist * dist;
+                da = quad < 1.0f ? 1.0f : 1.0f / quad;
+                dtl = normalized(disp);
+                to = make_ray(hpos, dtl);
+                max_t = dist;
+            } else {                                           // DirLight::shine (light.cu:72-77)
+                dtl = neg(L.v);
+                to = make_ray(hpos, dtl);
+                max_t = INFINITY;
+            }
+            rv = L.col;                                        // Light::attenuate (light.cu:29-61)
+            q = make_ray(at(to, THRESH), to.d);
+            dbg(P, me, 4);
+            phase = PH_SHADOW;
+            return;
+        }
+        acc = acc + fr[fidx].atten * summed;                   // scene.cu:127
+        advance();
+    };
+    auto light_done = [&](V4 att) {
+        const DLight L = S.lights[li];
+        V4 inc = (L.type == 0) ? da * att : att;
+        summed = summed + phong(S.mats[is.mat], is.norm, inc, fr[fidx].ray.d, dtl);
+        li++;
+        next_light();
+    };
+
+    if (valid) advance();
+
+    for (;;) {
+        const bool need = (phase == PH_NORMAL || phase == PH_SHADOW);
+        if (!__ballot(need)) break;
+        Hit h;
+        h.time = INFINITY; h.norm = is.norm; h.mat = is.mat; h.inst = -1; h.tri = -1;
+        bool hit = cast_ray(S, need, q, h, cnt);
+        if (!need) continue;
+        if (phase == PH_NORMAL) {
+            if (primary) { primary = false; if (hit) { hinst = h.inst; htri = h.tri; } }
+            if (!hit) { is.time = INFINITY; top--; advance(); continue; }
+            is.time = h.time; is.norm = h.norm; is.mat = h.mat;
+            Frame& f = fr[top];
+            fidx = top;
+            if (f.depth > 0) {                                 // scene.cu:109-121
+                if (f.in_obj) {
+                    const V4 kt = S.mats[is.mat].Kt;           // trans_atten (scene.cu:14-22): time^Kt
+                    f.atten = f.atten * v4(pow_ref(is.time, kt.x), pow_ref(is.time, kt.y),
+                                           pow_ref(is.time, kt.z), pow_ref(is.time, kt.w));
+                }
+                f.type = F_REFLECT;
+                f.hit_pt = at(f.ray, is.time);
+                f.last_mat = is.mat;
+                f.norm = is.norm;
+            } else {
+                top--;
+            }
+            const DMat& m = S.mats[is.mat];                    // illuminate (phong.cu:42-53)
+            summed = m.Ke + m.Ka * P.ambience;
+            hpos = at(fr[fidx].ray, is.time);
+            li = 0;
+            next_light();
+        } else {                                               // shadow segment result
+            if (!hit) { light_done(rv); continue; }
+            if (h.time > max_t) { light_done(rv); continue; }
+            const DMat& m = S.mats[h.mat];
+            if (!m.refractive) { light_done(v4(0, 0, 0, 0)); continue; }
+            if (dot(h.norm, q.d) > 0) {                        // calc_shadow_atten (light.cu:18-25)
+                rv = rv * v4(pow_ref(m.Kt.x, h.time), pow_ref(m.Kt.y, h.time), pow_ref(m.Kt.z, h.time),
+                             pow_ref(m.Kt.w, h.time));
+            }
+            q = make_ray(at(q, h.time), q.d);
+            max_t -= h.time;
+            dbg(P, me, 4);
+        }
+    }
+
+    if (valid) {
+        const float inv = (float)P.spp;
+        const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
+        // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
+        const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
+                             ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
+        const size_t p = P.compact ? (size_t)pr * P.W + px : (size_t)py * P.W + px;
+        if (P.rgba) P.rgba[p] = enc;
+        if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
+        if (P.hit_inst) P.hit_inst[p] = hinst;
+        if (P.hit_tri) P.hit_tri[p] = htri;
+    }
+    if (P.stats) {                                             // wave-reduced counters
+        unsigned long long v[4] = {cnt.rays, cnt.nodes, cnt.leaves, cnt.tris};
+        for (int i = 0; i < 4; i++) {
+            unsigned long long x = v[i];
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+            if (lane == 0 && x) atomicAdd(&P.stats[i], x);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// BVH build: ropt::gpu::BVH::BVH (bvh.cu:74-91) + create_boxes (raytracer.cu:54-74)
+// in one workgroup.  Output: heap-ordered nodes[1 .. 2n-1].
+// ---------------------------------------------------------------------------
+struct BvhArgs {
+    const DInst* insts; int n_inst;
+    const DMesh* meshes; int n_meshes;
+    const DTri* tris;
+    int n;                   // padded leaf count (power of two)
+    Box* boxes;              // scratch: n instance boxes
+    Box* tree;               // scratch: 2n-1 boxes, reference storage order
+    DNode* nodes;            // out: 2n entries (index 0 unused)
+};
+
+__global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
+    int* idx = reinterpret_cast<int*>(smem + sizeof(unsigned long long) * A.n);
+    Box* mbox = reinterpret_cast<Box*>(smem + 12 * (size_t)A.n);
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int n = A.n;
+
+    // mesh boxes: Trimesh::compute_bounding_box (trimesh.cu:21-32), sequential fit order
+    for (int m = tid; m < A.n_meshes; m += nt) {
+        Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
+        const DMesh mesh = A.meshes[m];
+        for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
+            fit_vertex(b, A.tris[t].a); fit_vertex(b, A.tris[t].b); fit_vertex(b, A.tris[t].c);
+        }
+        mbox[m] = from_local(b, mesh.pose);
+    }
+    __syncthreads();
+    // instance boxes + Morton keys (gen_morton, bvh.cu:20-32); padding is degenerate -> ULONG_MAX
+    for (int i = tid; i < n; i += nt) {
+        Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
+        if (i < A.n_inst) b = from_local(mbox[A.insts[i].mesh], A.insts[i].pose);
+        A.boxes[i] = b;
+        keys[i] = b.nd ? z_order(neg(box_center(b))) : ~0ull;
+        idx[i] = i;
+    }
+    __syncthreads();
+    // bitonic sort on (key, index): identical order to a stable sort by key
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < n; i += nt) {
+                int j = i ^ stride;
+                if (j > i) {
+                    bool up = (i & size) == 0;
+                    unsigned long long ki = keys[i], kj = keys[j];
+                    int ii = idx[i], ij = idx[j];
+                    bool gt = (ki > kj) || (ki == kj && ii > ij);
+                    if (gt == up) { keys[i] = kj; keys[j] = ki; idx[i] = ij; idx[j] = ii; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // reorder (bvh.cu:34-41) and pairwise level merges (bvh.cu:43-61)
+    for (int i = tid; i < n; i += nt) A.tree[i] = A.boxes[idx[i]];
+    __syncthreads();
+    int lvl = 0, size = n, out = n;
+    while (size >= 2) {
+        for (int i = tid; i < size / 2; i += nt) A.tree[out + i] = merge(A.tree[lvl + 2 * i], A.tree[lvl + 2 * i + 1]);
+        __syncthreads();
+        lvl += size; out += size / 2; size >>= 1;
+    }
+    // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
+    for (int k = tid + 1; k < 2 * n; k += nt) {
+        const int s = 2 * n - 1 - k;
+        const Box b = A.tree[s];
+        DNode d;
+        d.mnx = b.mn.x; d.mny = b.mn.y; d.mnz = b.mn.z; d.mxx = b.mx.x; d.mxy = b.mx.y; d.mxz = b.mx.z;
+        d.nd = b.nd;
+        d.inst = (k >= n) ? idx[s] : -1;
+        A.nodes[k] = d;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device KAT kernel (test hook): the same inline functions the trace kernel uses.
+// ---------------------------------------------------------------------------
+__global__ void kat_kernel(int op, int n, const float* a, const float* b, const float* c, float* of, int* oi,
+                           unsigned long long* ou) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    auto L3 = [](const float* p) { return v3(p[0], p[1], p[2]); };
+    auto S3 = [](float* p, V3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; };
+    switch (op) {
+        case 0: S3(of + 3 * i, normalized(L3(a + 3 * i))); break;
+        case 1: S3(of + 3 * i, cross(L3(a + 3 * i), L3(b + 3 * i))); break;
+        case 2: S3(of + 3 * i, reflect(L3(a + 3 * i), L3(b + 3 * i))); break;
+        case 3: { bool t; S3(of + 3 * i, refract(L3(a + 3 * i), L3(b + 3 * i), c[2 * i], c[2 * i + 1], t)); oi[i] = t; break; }
+        case 4: {
+            Q q{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]};
+            Pose e{};  // exercise the same Pose path the kernels use (incl. the identity specialisation)
+            e.identity = (__float_as_uint(q.i) == 0u && __float_as_uint(q.j) == 0u && __float_as_uint(q.k) == 0u &&
+                          __float_as_uint(q.r) == 0x3f800000u);
+            e.tn = qnormalized(q); e.ti = qinverse(q);
+            S3(of + 3 * i, vec_to_local(e, L3(b + 3 * i)));
+            break;
+        }
+        case 5: { Q r = qinverse(Q{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]}); of[4 * i] = r.i; of[4 * i + 1] = r.j; of[4 * i + 2] = r.k; of[4 * i + 3] = r.r; break; }
+        case 6: {
+            Q r = qmul(Q{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]}, Q{b[4 * i], b[4 * i + 1], b[4 * i + 2], b[4 * i + 3]});
+            of[4 * i] = r.i; of[4 * i + 1] = r.j; of[4 * i + 2] = r.k; of[4 * i + 3] = r.r; break;
+        }
+        case 7: {
+            const float* t = a + 9 * i;
+            V3 A = L3(t), B = L3(t + 3), C = L3(t + 6);
+            V3 pn = cross(B - A, C - A);
+            Ray r = make_ray(L3(b + 6 * i), L3(b + 6 * i + 3));
+            float tm = NAN, u = NAN, v = NAN;
+            bool h = tri_hit(A, B, C, normalized(pn), len(pn), r, tm, u, v);
+            oi[i] = h; of[3 * i] = h ? tm : NAN; of[3 * i + 1] = h ? u : NAN; of[3 * i + 2] = h ? v : NAN;
+            break;
+        }
+        case 8: { Ray r = make_ray(L3(a + 6 * i), L3(a + 6 * i + 3)); S3(of + 6 * i, r.o); S3(of + 6 * i + 3, r.d); break; }
+        case 9: ou[i] = z_order(L3(a + 3 * i)); break;
+        case 10: { float m[3][3]; to_mat3(Q{a[4 * i], a[4 * i + 1], a[4 * i + 2], a[4 * i + 3]}, m);
+                   for (int x = 0; x < 9; x++) of[9 * i + x] = m[x / 3][x % 3]; break; }
+        case 11: {
+            const float* bx = a + 7 * i;
+            Ray r = make_ray(L3(b + 6 * i), L3(b + 6 * i + 3));
+            oi[i] = bx[6] != 0 && box_hit(L3(bx), L3(bx + 3), r);
+            break;
+        }
+        case 12: of[i] = pow_ref(a[i], b[i]); break;
+        default: break;
+    }
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side: scene object and the C ABI
+// ===========================================================================
+struct rt_scene {
+    rt::Scene h;
+    bool finished = false;
+    int device = -1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // device buffers
+    DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
+    DLight* d_lights = nullptr; DNode* d_nodes = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
+    float2* d_spp = nullptr; int spp_cap = 0;
+    unsigned long long* d_stats = nullptr;
+    uint32_t* d_canvas = nullptr;
+    int* d_dbg = nullptr;
+    void* d_out[4] = {nullptr, nullptr, nullptr, nullptr};   // staging for host_outputs
+    std::vector<hipEvent_t> tev;      // timing=1 event triples (pool)
+    size_t tev_used = 0;
+    size_t d_out_px = 0;
+    int n_leaf = 0;
+    bool uploaded = false, bvh_valid = false;
+    std::vector<uint32_t> canvas;    // host framebuffer (Canvas buffer, canvas.cu:7)
+    ~rt_scene();
+};
+
+namespace {
+thread_local std::string g_err;
+thread_local int g_device = 0;
+
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return fail(RT_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); } while (0)
+
+template <class T> void dfree(T*& p) { if (p) { (void)hipFree(p); p = nullptr; } }
+
+int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
+    if (n_t <= 0) return 0;
+    int n = 1;
+    while (n < n_t) n <<= 1;
+    return n;
+}
+
+int upload(rt_scene* s) {
+    if (s->uploaded) return RT_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    s->device = g_device;
+    HIPCHK(hipSetDevice(s->device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, s->device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(RT_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
+    const rt::Scene& h = s->h;
+    auto up = [&](auto*& dst, const auto& vec) -> int {
+        using T = typename std::remove_reference<decltype(vec)>::type::value_type;
+        size_t bytes = std::max<size_t>(1, vec.size()) * sizeof(T);
+        HIPCHK(hipMalloc((void**)&dst, bytes));
+        if (!vec.empty()) HIPCHK(hipMemcpy(dst, vec.data(), vec.size() * sizeof(T), hipMemcpyHostToDevice));
+        return RT_OK;
+    };
+    int r;
+    if ((r = up(s->d_tris, h.d_tris)) || (r = up(s->d_meshes, h.d_meshes)) || (r = up(s->d_insts, h.d_insts)) ||
+        (r = up(s->d_mats, h.d_mats)) || (r = up(s->d_lights, h.d_lights)))
+        return r;
+    s->n_leaf = padded((int)h.d_insts.size());
+    if (s->n_leaf > BVH_MAX_LEAVES) return fail(RT_ERR_LIMIT, "more than 8192 padded instances: single-workgroup BVH build limit");
+    size_t nl = std::max(1, s->n_leaf);
+    HIPCHK(hipMalloc((void**)&s->d_nodes, 2 * nl * sizeof(DNode)));
+    HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
+    HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
+    HIPCHK(hipMalloc((void**)&s->d_stats, 4 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
+    s->uploaded = true;
+    return RT_OK;
+}
+
+int ensure_spp(rt_scene* s, int spp) {
+    if (spp <= s->spp_cap) return RT_OK;
+    int cap = std::max(spp, 64);
+    std::vector<float2> tab(cap);
+    for (int k = 0; k < cap; k++) rt::spp_offset(k, &tab[k].x, &tab[k].y);
+    dfree(s->d_spp);
+    HIPCHK(hipMalloc((void**)&s->d_spp, cap * sizeof(float2)));
+    HIPCHK(hipMemcpy(s->d_spp, tab.data(), cap * sizeof(float2), hipMemcpyHostToDevice));
+    s->spp_cap = cap;
+    return RT_OK;
+}
+
+int build_bvh(rt_scene* s, hipStream_t st) {
+    if (s->n_leaf == 0) { s->bvh_valid = true; return RT_OK; }
+    BvhArgs A;
+    A.insts = s->d_insts; A.n_inst = (int)s->h.d_insts.size();
+    A.meshes = s->d_meshes; A.n_meshes = (int)s->h.d_meshes.size();
+    A.tris = s->d_tris; A.n = s->n_leaf;
+    A.boxes = s->d_boxes; A.tree = s->d_tree; A.nodes = s->d_nodes;
+    size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
+    lds = (lds + 15) & ~size_t(15);
+    if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
+    hipLaunchKernelGGL(bvh_build_kernel, dim3(1), dim3(1024), lds, st, A);
+    HIPCHK(hipGetLastError());
+    s->bvh_valid = true;
+    return RT_OK;
+}
+
+SceneView view_of(const rt_scene* s, bool use_bvh) {
+    SceneView v;
+    v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
+    v.nodes = s->d_nodes; v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
+    v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
+    return v;
+}
+
+int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y) {
+    TraceParams P{};
+    const rt::Scene& h = s->h;
+    P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
+    P.W = h.cam.W; P.H = h.cam.H; P.row0 = o.row0; P.row_step = o.row_step;
+    P.n_rows = (P.H - o.row0 + o.row_step - 1) / o.row_step;
+    if (P.n_rows <= 0) return RT_OK;
+    P.compact = o.compact; P.spp = o.spp; P.depth = h.depth;
+    P.spp_off = s->d_spp;
+    P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
+    P.stats = s->d_stats; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
+    SceneView S = view_of(s, o.use_bvh != 0);
+    dim3 grid((P.W + 15) / 16, (P.n_rows + 15) / 16);
+    const int nf = h.depth + 1;                               // frames needed: depth + 1 (<= MAX_FRAMES)
+    if (nf <= 1) hipLaunchKernelGGL(trace_kernel<1>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    else if (nf <= 3) hipLaunchKernelGGL(trace_kernel<3>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    else hipLaunchKernelGGL(trace_kernel<MAX_FRAMES>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    HIPCHK(hipGetLastError());
+    return RT_OK;
+}
+
+#define CHECK_SCENE(s) do { if (!(s)) return fail(RT_ERR_ARG, "null scene"); } while (0)
+#define CHECK_BUILDING(s) do { CHECK_SCENE(s); if ((s)->finished) return fail(RT_ERR_STATE, "scene already finished"); } while (0)
+#define CHECK_FINISHED(s) do { CHECK_SCENE(s); if (!(s)->finished) return fail(RT_ERR_STATE, "scene not finished (call rt_builder_finish)"); } while (0)
+
+rt::Material mat_from(const float* m) {
+    rt::Material r;
+    r.Ke = v4(m[0], m[1], m[2], m[3]); r.Ka = v4(m[4], m[5], m[6], m[7]); r.Kd = v4(m[8], m[9], m[10], m[11]);
+    r.Ks = v4(m[12], m[13], m[14], m[15]); r.Kt = v4(m[16], m[17], m[18], m[19]); r.Kr = v4(m[20], m[21], m[22], m[23]);
+    r.alpha = m[24]; r.eta = m[25];
+    return r;
+}
+
+void invalidate(rt_scene* s) { s->bvh_valid = false; }
+
+}  // namespace
+
+rt_scene::~rt_scene() {
+    if (uploaded) (void)hipSetDevice(device);
+    dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights); dfree(d_nodes);
+    dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
+    for (auto& p : d_out) dfree(p);
+    for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : tev) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_device_count(int* count) {
+    if (!count) return fail(RT_ERR_ARG, "null count");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RT_OK;
+}
+
+int rt_set_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    if (device < 0 || device >= n) return fail(RT_ERR_ARG, "device index out of range");
+    g_device = device;
+    HIPCHK(hipSetDevice(device));
+    return RT_OK;
+}
+
+int rt_spp_offset(int k, float* dx, float* dy) {
+    if (k < 0 || !dx || !dy) return fail(RT_ERR_ARG, "bad arguments");
+    rt::spp_offset(k, dx, dy);
+    return RT_OK;
+}
+
+int rt_scene_load_json(const char* path, int width, int height, rt_scene** out) {
+    if (!path || !out) return fail(RT_ERR_ARG, "null argument");
+    std::unique_ptr<rt_scene> s(new rt_scene);
+    std::string err;
+    int r = rt::load_cube_world(path, width, height, &s->h, &err);
+    if (r == -2) return fail(RT_ERR_IO, err);
+    if (r != 0) return fail(RT_ERR_PARSE, err);
+    s->finished = true;
+    s->canvas.assign((size_t)s->h.cam.W * s->h.cam.H, 0u);
+    *out = s.release();
+    return RT_OK;
+}
+
+int rt_scene_create(const char* atlas, rt_scene** out) {
+    if (!out) return fail(RT_ERR_ARG, "null argument");
+    rt_scene* s = new rt_scene;
+    s->h.atlas = atlas ? atlas : "";
+    *out = s;
+    return RT_OK;
+}
+
+int rt_scene_free(rt_scene* s) { delete s; return RT_OK; }
+
+int rt_builder_add_vertex(rt_scene* s, float x, float y, float z, int* idx) {
+    CHECK_BUILDING(s);
+    int i = s->h.add_vertex(v3(x, y, z));
+    if (idx) *idx = i;
+    return RT_OK;
+}
+int rt_builder_create_mesh(rt_scene* s, const float* pos, const float* q, int* mesh) {
+    CHECK_BUILDING(s);
+    int m = s->h.create_mesh(pos ? v3(pos[0], pos[1], pos[2]) : v3(0, 0, 0), q ? Q{q[0], q[1], q[2], q[3]} : Q{0, 0, 0, 1});
+    if (mesh) *mesh = m;
+    return RT_OK;
+}
+int rt_builder_add_triangle(rt_scene* s, int mesh, int i0, int i1, int i2, const float* mat) {
+    CHECK_BUILDING(s);
+    if (!mat) return fail(RT_ERR_ARG, "null material");
+    if (mesh < 0 || mesh >= (int)s->h.meshes.size()) return fail(RT_ERR_ARG, "mesh index out of range");
+    int nv = (int)s->h.verts.size();
+    if (i0 < 0 || i1 < 0 || i2 < 0 || i0 >= nv || i1 >= nv || i2 >= nv) return fail(RT_ERR_ARG, "vertex index out of range");
+    s->h.add_triangle(mesh, i0, i1, i2, s->h.add_material(mat_from(mat)));
+    return RT_OK;
+}
+int rt_builder_add_trans(rt_scene* s, int mesh, int* trans) {
+    CHECK_BUILDING(s);
+    if (mesh < 0 || mesh >= (int)s->h.meshes.size()) return fail(RT_ERR_ARG, "mesh index out of range");
+    int t = s->h.add_trans(mesh);
+    if (trans) *trans = t;
+    return RT_OK;
+}
+int rt_builder_set_trans(rt_scene* s, int t, const float* pos, const float* q) {
+    CHECK_SCENE(s);
+    if (t < 0 || t >= (int)s->h.insts.size()) return fail(RT_ERR_ARG, "transformation index out of range");
+    if (pos) s->h.insts[t].pos = v3(pos[0], pos[1], pos[2]);
+    if (q) s->h.insts[t].rot = Q{q[0], q[1], q[2], q[3]};
+    if (s->finished) {   // instances moved after finishing: refresh the flat copy and the device copy
+        s->h.d_insts[t].pose = make_pose(s->h.insts[t].rot, s->h.insts[t].pos);
+        if (s->uploaded) HIPCHK(hipMemcpy(s->d_insts + t, &s->h.d_insts[t], sizeof(DInst), hipMemcpyHostToDevice));
+        invalidate(s);
+    }
+    return RT_OK;
+}
+int rt_builder_build_cube(rt_scene* s, float scale, const float* mat, int* mesh) {
+    CHECK_BUILDING(s);
+    if (!mat) return fail(RT_ERR_ARG, "null material");
+    int m = s->h.build_cube(scale, mat_from(mat));
+    if (mesh) *mesh = m;
+    return RT_OK;
+}
+int rt_builder_add_point_light(rt_scene* s, const float* pos, const float* col) {
+    CHECK_BUILDING(s);
+    if (!pos || !col) return fail(RT_ERR_ARG, "null argument");
+    s->h.add_point_light(v3(pos[0], pos[1], pos[2]), v4(col[0], col[1], col[2], col[3]));
+    return RT_OK;
+}
+int rt_builder_add_directional_light(rt_scene* s, const float* dir, const float* col) {
+    CHECK_BUILDING(s);
+    if (!dir || !col) return fail(RT_ERR_ARG, "null argument");
+    s->h.add_directional_light(v3(dir[0], dir[1], dir[2]), v4(col[0], col[1], col[2], col[3]));
+    return RT_OK;
+}
+int rt_builder_finish(rt_scene* s, int W, int H, float fov, float unit, const float* cpos, const float* cq,
+                      const float* da, const float* amb, int depth) {
+    CHECK_BUILDING(s);
+    if (W <= 0 || H <= 0 || !(unit > 0)) return fail(RT_ERR_ARG, "bad canvas/camera parameters");
+    s->h.set_camera(W, H, fov, unit);
+    if (cpos) s->h.cam.pos = v3(cpos[0], cpos[1], cpos[2]);
+    if (cq) s->h.cam.rot = Q{cq[0], cq[1], cq[2], cq[3]};
+    if (da) s->h.dist_atten = v3(da[0], da[1], da[2]);
+    if (amb) s->h.ambience = v4(amb[0], amb[1], amb[2], amb[3]);
+    s->h.depth = depth;
+    std::string err;
+    if (s->h.flatten(&err) != 0) return fail(RT_ERR_PARSE, err);
+    s->finished = true;
+    s->canvas.assign((size_t)W * H, 0u);
+    return RT_OK;
+}
+
+int rt_scene_info(const rt_scene* s, int32_t* c) {
+    CHECK_FINISHED(s);
+    if (!c) return fail(RT_ERR_ARG, "null argument");
+    const rt::Scene& h = s->h;
+    c[0] = h.cam.W; c[1] = h.cam.H; c[2] = (int)h.verts.size(); c[3] = (int)h.tris.size(); c[4] = (int)h.meshes.size();
+    c[5] = (int)h.insts.size(); c[6] = (int)h.d_lights.size(); c[7] = (int)h.points.size(); c[8] = h.depth;
+    c[9] = (int)h.mats.size();
+    return RT_OK;
+}
+
+int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
+    CHECK_FINISHED(s);
+    const rt::Scene& h = s->h;
+    std::vector<float> f;
+    std::vector<int32_t> iv;
+    switch (what) {
+        case RT_EXPORT_VERTICES: for (auto& v : h.verts) { f.push_back(v.x); f.push_back(v.y); f.push_back(v.z); } break;
+        case RT_EXPORT_NORMALS: f = h.verts_norm; break;
+        case RT_EXPORT_TRIS: for (auto& t : h.tris) { iv.push_back(t.i0); iv.push_back(t.i1); iv.push_back(t.i2); iv.push_back(t.mat); } break;
+        case RT_EXPORT_MATERIALS:
+            for (auto& m : h.mats) {
+                for (const V4* v : {&m.Ke, &m.Ka, &m.Kd, &m.Ks, &m.Kt, &m.Kr}) { f.push_back(v->x); f.push_back(v->y); f.push_back(v->z); f.push_back(v->w); }
+                f.push_back(m.alpha); f.push_back(m.eta);
+            }
+            break;
+        case RT_EXPORT_INSTANCES:
+            for (auto& t : h.insts) { f.insert(f.end(), {t.rot.i, t.rot.j, t.rot.k, t.rot.r, t.pos.x, t.pos.y, t.pos.z}); }
+            break;
+        case RT_EXPORT_INST_MESH: for (auto& t : h.insts) iv.push_back(t.mesh); break;
+        case RT_EXPORT_LIGHTS:
+            for (auto& l : h.d_lights) f.insert(f.end(), {l.v.x, l.v.y, l.v.z, (float)l.type, l.col.x, l.col.y, l.col.z, l.col.w});
+            break;
+        case RT_EXPORT_CAMERA: {
+            const DCamera& c = h.d_cam;
+            f = {c.pos.x, c.pos.y, c.pos.z, h.cam.rot.i, h.cam.rot.j, h.cam.rot.k, h.cam.rot.r, c.near_, c.unit, c.W, c.H,
+                 c.r.x, c.r.y, c.r.z, c.u.x, c.u.y, c.u.z, c.f.x, c.f.y, c.f.z, 0.0f};
+            break;
+        }
+        case RT_EXPORT_ENV:
+            f = {h.dist_atten.x, h.dist_atten.y, h.dist_atten.z, h.ambience.x, h.ambience.y, h.ambience.z, h.ambience.w};
+            break;
+        default: return fail(RT_ERR_ARG, "unknown export");
+    }
+    size_t bytes = f.size() * 4 + iv.size() * 4;
+    if (!dst || cap < (int64_t)bytes) return fail(RT_ERR_ARG, "destination too small");
+    if (!f.empty()) memcpy(dst, f.data(), f.size() * 4);
+    if (!iv.empty()) memcpy(dst, iv.data(), iv.size() * 4);
+    return RT_OK;
+}
+
+int rt_camera_get(const rt_scene* s, float* pos, float* q) {
+    CHECK_SCENE(s);
+    if (pos) { pos[0] = s->h.cam.pos.x; pos[1] = s->h.cam.pos.y; pos[2] = s->h.cam.pos.z; }
+    if (q) { q[0] = s->h.cam.rot.i; q[1] = s->h.cam.rot.j; q[2] = s->h.cam.rot.k; q[3] = s->h.cam.rot.r; }
+    return RT_OK;
+}
+int rt_camera_set(rt_scene* s, const float* pos, const float* q) {
+    CHECK_FINISHED(s);
+    if (pos) s->h.cam.pos = v3(pos[0], pos[1], pos[2]);
+    if (q) s->h.cam.rot = Q{q[0], q[1], q[2], q[3]};
+    s->h.update_camera_basis();
+    return RT_OK;
+}
+int rt_camera_translate(rt_scene* s, const float* d) {           // entity.h:53-56: translate_global(vec_to_local(dp))
+    CHECK_FINISHED(s);
+    if (!d) return fail(RT_ERR_ARG, "null argument");
+    s->h.cam.pos = s->h.cam.pos + qrot(s->h.cam.rot, v3(d[0], d[1], d[2]));
+    s->h.update_camera_basis();
+    return RT_OK;
+}
+int rt_camera_rotate(rt_scene* s, const float* dq) {             // entity.h:63-65: o = dr * o
+    CHECK_FINISHED(s);
+    if (!dq) return fail(RT_ERR_ARG, "null argument");
+    s->h.cam.rot = qmul(Q{dq[0], dq[1], dq[2], dq[3]}, s->h.cam.rot);
+    s->h.update_camera_basis();
+    return RT_OK;
+}
+int rt_camera_axes(const rt_scene* s, float* r, float* u, float* f) {
+    CHECK_FINISHED(s);
+    const DCamera& c = s->h.d_cam;
+    if (r) { r[0] = c.r.x; r[1] = c.r.y; r[2] = c.r.z; }
+    if (u) { u[0] = c.u.x; u[1] = c.u.y; u[2] = c.u.z; }
+    if (f) { f[0] = c.f.x; f[1] = c.f.y; f[2] = c.f.z; }
+    return RT_OK;
+}
+int rt_env_set(rt_scene* s, const float* amb, const float* da, int depth) {
+    CHECK_FINISHED(s);
+    if (depth < 0 || depth >= MAX_FRAMES) return fail(RT_ERR_ARG, "depth must be in [0, 9]");
+    if (amb) s->h.ambience = v4(amb[0], amb[1], amb[2], amb[3]);
+    if (da) s->h.dist_atten = v3(da[0], da[1], da[2]);
+    s->h.depth = depth;
+    return RT_OK;
+}
+
+void rt_render_opts_default(rt_render_opts* o) {
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->spp = 1; o->use_bvh = 1; o->rebuild_bvh = 1; o->row0 = 0; o->row_step = 1; o->kernel_dim = 16; o->sync = 1;
+}
+
+int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
+    CHECK_FINISHED(s);
+    if (!o) return fail(RT_ERR_ARG, "null options");
+    if (o->spp < 1 || o->row_step < 1 || o->row0 < 0) return fail(RT_ERR_ARG, "spp >= 1, row_step >= 1, row0 >= 0 required");
+    int r;
+    if ((r = upload(s)) != RT_OK) return r;
+    HIPCHK(hipSetDevice(s->device));
+    if ((r = ensure_spp(s, o->spp)) != RT_OK) return r;
+    hipStream_t st = o->stream ? (hipStream_t)o->stream : s->stream;
+    const bool timed = stats != nullptr;
+    hipEvent_t* te = nullptr;
+    if (o->timing) {
+        if (s->tev_used + 3 > s->tev.size()) {
+            if (s->tev.size() >= 3 * 4096) return fail(RT_ERR_STATE, "too many timed frames pending: call rt_timing_collect");
+            for (int i = 0; i < 3 * 64; i++) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); s->tev.push_back(e); }
+        }
+        te = &s->tev[s->tev_used];
+        s->tev_used += 3;
+        HIPCHK(hipEventRecord(te[0], st));
+    }
+    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
+    if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
+        if ((r = build_bvh(s, st)) != RT_OK) return r;
+    }
+    if (timed) HIPCHK(hipEventRecord(s->ev[1], st));
+    if (te) HIPCHK(hipEventRecord(te[1], st));
+    rt_render_opts oo = *o;
+    const size_t W = s->h.cam.W, H = s->h.cam.H;
+    const size_t n_rows = (H > (size_t)o->row0) ? (H - o->row0 + o->row_step - 1) / o->row_step : 0;
+    const size_t out_px = o->compact ? n_rows * W : W * H;
+    if (o->host_outputs) {                                   // stage through device buffers
+        if (s->d_out_px < W * H) {
+            for (auto& p : s->d_out) dfree(p);
+            HIPCHK(hipMalloc(&s->d_out[0], W * H * 4)); HIPCHK(hipMalloc(&s->d_out[1], W * H * 16));
+            HIPCHK(hipMalloc(&s->d_out[2], W * H * 4)); HIPCHK(hipMalloc(&s->d_out[3], W * H * 4));
+            s->d_out_px = W * H;
+        }
+        oo.rgba = o->rgba ? (uint32_t*)s->d_out[0] : nullptr;
+        oo.radiance = o->radiance ? (float*)s->d_out[1] : nullptr;
+        oo.hit_inst = o->hit_inst ? (int32_t*)s->d_out[2] : nullptr;
+        oo.hit_tri = o->hit_tri ? (int32_t*)s->d_out[3] : nullptr;
+    }
+    uint32_t* rgba = oo.rgba ? oo.rgba : s->d_canvas;
+    if ((r = launch_trace(s, oo, st, rgba, nullptr, -1, -1)) != RT_OK) return r;
+    if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
+    if (te) HIPCHK(hipEventRecord(te[2], st));
+    if (o->sync || timed || o->host_outputs) HIPCHK(hipStreamSynchronize(st));
+    if (o->host_outputs) {
+        if (o->rgba) HIPCHK(hipMemcpy(o->rgba, oo.rgba, out_px * 4, hipMemcpyDeviceToHost));
+        if (o->radiance) HIPCHK(hipMemcpy(o->radiance, oo.radiance, out_px * 16, hipMemcpyDeviceToHost));
+        if (o->hit_inst) HIPCHK(hipMemcpy(o->hit_inst, oo.hit_inst, out_px * 4, hipMemcpyDeviceToHost));
+        if (o->hit_tri) HIPCHK(hipMemcpy(o->hit_tri, oo.hit_tri, out_px * 4, hipMemcpyDeviceToHost));
+    }
+    if (timed) {
+        unsigned long long v[4];
+        HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
+        stats->rays = v[0]; stats->nodes = v[1]; stats->leaves = v[2]; stats->tri_tests = v[3];
+        float a = 0, b = 0;
+        HIPCHK(hipEventElapsedTime(&a, s->ev[0], s->ev[1]));
+        HIPCHK(hipEventElapsedTime(&b, s->ev[1], s->ev[2]));
+        stats->bvh_ms = a; stats->trace_ms = b;
+    }
+    return RT_OK;
+}
+
+int rt_timing_collect(rt_scene* s, double* bvh_ms, double* trace_ms, int* n) {
+    CHECK_FINISHED(s);
+    double a = 0, b = 0;
+    for (size_t i = 0; i + 3 <= s->tev_used; i += 3) {
+        HIPCHK(hipEventSynchronize(s->tev[i + 2]));
+        float x = 0, y = 0;
+        HIPCHK(hipEventElapsedTime(&x, s->tev[i], s->tev[i + 1]));
+        HIPCHK(hipEventElapsedTime(&y, s->tev[i + 1], s->tev[i + 2]));
+        a += x; b += y;
+    }
+    if (bvh_ms) *bvh_ms = a;
+    if (trace_ms) *trace_ms = b;
+    if (n) *n = (int)(s->tev_used / 3);
+    s->tev_used = 0;
+    return RT_OK;
+}
+
+int rt_update_scene(rt_scene* s, int kernel_dim, int optimize) {    // raytracer.cu:102-120
+    CHECK_FINISHED(s);
+    if (kernel_dim <= 0) return fail(RT_ERR_ARG, "kernel_dim must be positive");
+    rt_render_opts o;
+    rt_render_opts_default(&o);
+    o.use_bvh = optimize ? 1 : 0; o.rebuild_bvh = 1; o.kernel_dim = kernel_dim; o.sync = 1;
+    int r = rt_render(s, &o, nullptr);
+    if (r != RT_OK) return r;
+    HIPCHK(hipMemcpy(s->canvas.data(), s->d_canvas, s->canvas.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_canvas_read(const rt_scene* s, uint32_t* dst, int64_t n) {
+    CHECK_FINISHED(s);
+    if (!dst || n < (int64_t)s->canvas.size()) return fail(RT_ERR_ARG, "destination too small");
+    memcpy(dst, s->canvas.data(), s->canvas.size() * sizeof(uint32_t));
+    return RT_OK;
+}
+const uint32_t* rt_canvas_host_ptr(const rt_scene* s) { return s ? s->canvas.data() : nullptr; }
+int rt_canvas_get_color(const rt_scene* s, int x, int y, uint8_t* c) {
+    CHECK_FINISHED(s);
+    if (!c || x < 0 || y < 0 || x >= s->h.cam.W || y >= s->h.cam.H) return fail(RT_ERR_ARG, "pixel out of range");
+    uint32_t e = s->canvas[(size_t)y * s->h.cam.W + x];                  // Color::from_encoding (color.cu:28-34)
+    c[0] = (uint8_t)(e >> 24); c[1] = (uint8_t)(e >> 16); c[2] = (uint8_t)(e >> 8); c[3] = (uint8_t)e;
+    return RT_OK;
+}
+
+int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // raytracer.cu:91-100
+    CHECK_FINISHED(s);
+    if (x < 0 || y < 0 || x >= s->h.cam.W || y >= s->h.cam.H) return fail(RT_ERR_ARG, "pixel out of range");
+    int r;
+    if ((r = upload(s)) != RT_OK) return r;
+    HIPCHK(hipSetDevice(s->device));
+    if ((r = ensure_spp(s, 1)) != RT_OK) return r;
+    if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+    HIPCHK(hipMemsetAsync(s->d_dbg, 0, 4096 * sizeof(int), s->stream));
+    rt_render_opts o;
+    rt_render_opts_default(&o);
+    o.row0 = y; o.row_step = s->h.cam.H;                                  // just the row of (x, y)
+    if ((r = launch_trace(s, o, s->stream, s->d_canvas, s->d_dbg, x, y)) != RT_OK) return r;
+    std::vector<int> log(4096);
+    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipMemcpy(log.data(), s->d_dbg, log.size() * sizeof(int), hipMemcpyDeviceToHost));
+    static const char* names[] = {"", "shooting a ray", "preparing to shoot a reflection ray",
+                                  "preparing to shoot a refraction ray", "shooting shadow ray"};
+    std::string out;
+    int n = std::min(log[0], 4094);
+    for (int i = 0; i < n; i++) { int e = log[2 + i]; if (e >= 1 && e <= 4) { out += names[e]; out += '\n'; } }
+    if (buf && cap > 0) { size_t m = std::min<size_t>(out.size(), (size_t)cap - 1); memcpy(buf, out.data(), m); buf[m] = 0; }
+    return RT_OK;
+}
+
+int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2, float* of, int32_t* oi,
+                  uint64_t* ou) {
+    static const char* ops[] = {"normalize3", "cross", "reflect", "refract", "quat_rotate", "quat_inverse", "quat_mul",
+                                "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow"};
+    // per-op sizes (floats): in0, in1, in2, out_f, out_i, out_u per element
+    static const int sz[][6] = {{3, 0, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 2, 3, 1, 0},
+                                {4, 3, 0, 3, 0, 0}, {4, 0, 0, 4, 0, 0}, {4, 4, 0, 4, 0, 0}, {9, 6, 0, 3, 1, 0},
+                                {6, 0, 0, 6, 0, 0}, {3, 0, 0, 0, 0, 1}, {4, 0, 0, 9, 0, 0}, {7, 6, 0, 0, 1, 0},
+                                {1, 1, 0, 1, 0, 0}};
+    if (!op || n <= 0) return fail(RT_ERR_ARG, "bad arguments");
+    int k = -1;
+    for (int i = 0; i < (int)(sizeof ops / sizeof *ops); i++) if (!strcmp(op, ops[i])) k = i;
+    if (k < 0) return fail(RT_ERR_ARG, std::string("unknown op ") + op);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    HIPCHK(hipSetDevice(g_device));
+    const float* hin[3] = {in0, in1, in2};
+    float* din[3] = {nullptr, nullptr, nullptr};
+    float* dof = nullptr; int* doi = nullptr; unsigned long long* dou = nullptr;
+    for (int i = 0; i < 3; i++)
+        if (sz[k][i]) {
+            if (!hin[i]) return fail(RT_ERR_ARG, "missing input");
+            HIPCHK(hipMalloc((void**)&din[i], (size_t)n * sz[k][i] * 4));
+            HIPCHK(hipMemcpy(din[i], hin[i], (size_t)n * sz[k][i] * 4, hipMemcpyHostToDevice));
+        }
+    if (sz[k][3]) HIPCHK(hipMalloc((void**)&dof, (size_t)n * sz[k][3] * 4));
+    if (sz[k][4]) HIPCHK(hipMalloc((void**)&doi, (size_t)n * 4));
+    if (sz[k][5]) HIPCHK(hipMalloc((void**)&dou, (size_t)n * 8));
+    hipLaunchKernelGGL(kat_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, k, n, din[0], din[1], din[2], dof, doi, dou);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    if (sz[k][3] && of) HIPCHK(hipMemcpy(of, dof, (size_t)n * sz[k][3] * 4, hipMemcpyDeviceToHost));
+    if (sz[k][4] && oi) HIPCHK(hipMemcpy(oi, doi, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (sz[k][5] && ou) HIPCHK(hipMemcpy(ou, dou, (size_t)n * 8, hipMemcpyDeviceToHost));
+    for (auto p : din) if (p) (void)hipFree(p);
+    if (dof) (void)hipFree(dof);
+    if (doi) (void)hipFree(doi);
+    if (dou) (void)hipFree(dou);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,236 @@
+// rt_math.h — bit-exact float32 math of the reference's raymath layer, usable on
+// the host (scene preparation) and on gfx950 (kernels).
+//
+// Semantics follow include/raymath/linear.h and geometry.h of
+// wtzhang23/gpu-ray-tracer operand-for-operand, because the renderer's integer
+// outputs (hit instance / triangle) depend on last-ulp comparisons (the 1e-5
+// barycentric tolerance, strict `<` on hit times).  Build rules that make this
+// hold: -ffp-contract=off everywhere, no fast-math, HIP's default correctly
+// rounded f32 division and sqrt, f32 denormals preserved (gfx950 default).
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#define RT_HD inline
+#endif
+
+namespace rtm {
+
+constexpr float THRESH = 1e-5f;   // rmath::THRESHOLD (linear.h:15): a double holding 1e-5f
+
+struct V3 { float x, y, z; };
+struct V4 { float x, y, z, w; };
+struct Q { float i, j, k, r; };   // geometry.h: inner = {i, j, k, r}
+
+RT_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+RT_HD V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RT_HD V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+// scalar * vector multiplies each coordinate by the scalar (linear.h:100-106, 132-137)
+RT_HD V3 operator*(float c, V3 v) { return v3(v.x * c, v.y * c, v.z * c); }
+RT_HD V3 neg(V3 v) { return (-1.0f) * v; }                           // (T)-1 * vec (linear.h:139-142)
+RT_HD float dot(V3 a, V3 b) {                                       // linear.h:197-205: 0 + x*x + ...
+    float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s;
+}
+RT_HD float len(V3 v) { return sqrtf(dot(v, v)); }
+RT_HD V3 normalized(V3 v) {                                         // linear.h:159-167
+    float l = len(v);
+    if (l > THRESH) return (1 / l) * v;
+    return v3(0.0f, 0.0f, 0.0f);
+}
+RT_HD V3 cross(V3 a, V3 b) {                                        // linear.h:207-215
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+RT_HD V4 v4(float x, float y, float z, float w) { return V4{x, y, z, w}; }
+RT_HD V4 operator+(V4 a, V4 b) { return v4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+RT_HD V4 operator*(V4 a, V4 b) { return v4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w); }
+RT_HD V4 operator*(float c, V4 v) { return v4(v.x * c, v.y * c, v.z * c, v.w * c); }
+RT_HD float dot4(V4 a, V4 b) {
+    float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; s += a.w * b.w; return s;
+}
+
+RT_HD V3 reflect(V3 dir, V3 nrm) {                                   // linear.h:217-226
+    float d_len = len(dir);
+    V3 dn = normalized(dir), nn = normalized(nrm);
+    V3 proj = dot(dn, nn) * nn;
+    return d_len * normalized(dn - 2.0f * proj);
+}
+RT_HD V3 refract(V3 dir, V3 nrm, float from, float to, bool& tir) {  // linear.h:228-243
+    float d_len = len(dir);
+    V3 dn = normalized(dir), nn = normalized(nrm);
+    float ratio = from / to;
+    float cosi = dot(dn, nn);
+    float sint_2 = ratio * ratio * (1 - cosi * cosi);
+    if (sint_2 > 1) { tir = true; return d_len * reflect(dn, nn); }
+    tir = false;
+    return d_len * (ratio * dn + (ratio * cosi - sqrtf(1 - sint_2)) * nn);
+}
+
+// ---- quaternions (geometry.h:17-199) ----
+RT_HD V4 qv(Q q) { return v4(q.i, q.j, q.k, q.r); }
+RT_HD Q qnormalized(Q q) {
+    float l = sqrtf(dot4(qv(q), qv(q)));
+    if (l > THRESH) { float c = 1 / l; return Q{q.i * c, q.j * c, q.k * c, q.r * c}; }
+    return Q{0.0f, 0.0f, 0.0f, 0.0f};
+}
+RT_HD Q qinverse(Q q) {
+    float sq = dot4(qv(q), qv(q));
+    if (sq < THRESH) return Q{0.0f, 0.0f, 0.0f, 0.0f};
+    float inv = 1 / sq;
+    return Q{q.i * -inv, q.j * -inv, q.k * -inv, q.r * inv};
+}
+RT_HD Q qmul(Q a, Q b) {
+    return Q{a.i * b.r + a.r * b.i + a.j * b.k - a.k * b.j,
+             a.j * b.r + a.r * b.j + a.k * b.i - a.i * b.k,
+             a.k * b.r + a.r * b.k + a.i * b.j - a.j * b.i,
+             a.r * b.r - a.i * b.i - a.j * b.j - a.k * b.k};
+}
+// Quat * Vec3 with the two quaternion-only factors precomputed:
+//   qn = normalized(q), qi = inverse(q)       (geometry.h:176-181)
+RT_HD V3 qrot_pre(Q qn, Q qi, V3 v) {
+    float length = len(v);
+    Q p = qmul(qmul(qn, Q{v.x, v.y, v.z, 0.0f}), qi);
+    return length * normalized(v3(p.i, p.j, p.k));
+}
+RT_HD V3 qrot(Q q, V3 v) { return qrot_pre(qnormalized(q), qinverse(q), v); }
+
+// Exact specialisation of qrot_pre for q == (0,0,0,1) or its inverse (-0,-0,-0,1)
+// (every pose in the cube world).  Proof sketch: both
+// quaternion products return the input coordinates unchanged except that a
+// zero comes back as +0; `x + 0.0f` performs exactly that canonicalisation
+// and is not folded without fast-math.  Then |v| * normalize(v') follows.
+RT_HD V3 qrot_identity(V3 v) {
+    float length = len(v);
+    V3 c = v3(v.x + 0.0f, v.y + 0.0f, v.z + 0.0f);
+    return length * normalized(c);
+}
+
+// ---- entity pose (entity.cu:5-37) with precomputed quaternion factors ----
+struct Pose {
+    V3 p;
+    int identity;   // 1 when o == (0,0,0,1) bitwise: use qrot_identity
+    Q tn, ti;       // to_local:   normalized(o),          inverse(o)
+    Q fn, fi;       // from_local: normalized(inverse(o)), inverse(inverse(o))
+};
+RT_HD V3 vec_to_local(const Pose& e, V3 v) { return e.identity ? qrot_identity(v) : qrot_pre(e.tn, e.ti, v); }
+RT_HD V3 vec_from_local(const Pose& e, V3 v) { return e.identity ? qrot_identity(v) : qrot_pre(e.fn, e.fi, v); }
+RT_HD V3 point_to_local(const Pose& e, V3 v) { return vec_to_local(e, v - e.p); }
+RT_HD V3 point_from_local(const Pose& e, V3 v) { return vec_from_local(e, v) + e.p; }
+
+inline bool bits_eq(float a, float b) { union { float f; uint32_t u; } x{a}, y{b}; return x.u == y.u; }
+inline Pose make_pose(Q o, V3 p) {
+    Pose e;
+    e.p = p;
+    e.identity = bits_eq(o.i, 0.0f) && bits_eq(o.j, 0.0f) && bits_eq(o.k, 0.0f) && bits_eq(o.r, 1.0f);
+    e.tn = qnormalized(o); e.ti = qinverse(o);
+    Q inv = qinverse(o);
+    e.fn = qnormalized(inv); e.fi = qinverse(inv);
+    return e;
+}
+
+// ---- rays (geometry.h:201-223) ----
+struct Ray { V3 o, d; };
+RT_HD Ray make_ray(V3 o, V3 d) { return Ray{o, normalized(d)}; }
+RT_HD V3 at(const Ray& r, float t) { return r.o + t * r.d; }
+
+// ---- bounding boxes (bounding_box.cu:5-104) ----
+struct Box { V3 mn, mx; int nd; };
+RT_HD void fit_vertex(Box& b, V3 v) {
+    if (!b.nd) { b.mn = v; b.mx = v; b.nd = 1; return; }
+    if (v.x < b.mn.x) b.mn.x = v.x;
+    if (v.x > b.mx.x) b.mx.x = v.x;
+    if (v.y < b.mn.y) b.mn.y = v.y;
+    if (v.y > b.mx.y) b.mx.y = v.y;
+    if (v.z < b.mn.z) b.mn.z = v.z;
+    if (v.z > b.mx.z) b.mx.z = v.z;
+}
+RT_HD Box merge(const Box& a, const Box& b) {
+    Box r = a;
+    if (!r.nd) return b;
+    if (!b.nd) return r;
+    if (r.mn.x > b.mn.x) r.mn.x = b.mn.x;
+    if (r.mx.x < b.mx.x) r.mx.x = b.mx.x;
+    if (r.mn.y > b.mn.y) r.mn.y = b.mn.y;
+    if (r.mx.y < b.mx.y) r.mx.y = b.mx.y;
+    if (r.mn.z > b.mn.z) r.mn.z = b.mn.z;
+    if (r.mx.z < b.mx.z) r.mx.z = b.mx.z;
+    return r;
+}
+RT_HD Box from_local(const Box& a, const Pose& e) {
+    Box r; r.nd = 0; r.mn = r.mx = v3(0.0f, 0.0f, 0.0f);
+    if (!a.nd) return r;
+    fit_vertex(r, point_from_local(e, a.mn));
+    fit_vertex(r, point_from_local(e, a.mx));
+    return r;
+}
+// Kay–Kajiya slab test, bounding_box.cu:62-104 (true divisions; zero-direction axes skipped)
+RT_HD bool slab_axis(float mn, float mx, float o, float d, float& tmin, float& tmax) {
+    if (d == 0) return true;
+    float tn = (mn - o) / d;
+    float tf = (mx - o) / d;
+    if (tn > tf) { float t = tn; tn = tf; tf = t; }
+    if (tn > tmin) tmin = tn;
+    if (tf < tmax) tmax = tf;
+    return !(tmin > tmax || tmax < THRESH);
+}
+RT_HD bool box_hit(V3 mn, V3 mx, const Ray& r) {
+    float tmin = -INFINITY, tmax = INFINITY;
+    if (!slab_axis(mn.x, mx.x, r.o.x, r.d.x, tmin, tmax)) return false;
+    if (!slab_axis(mn.y, mx.y, r.o.y, r.d.y, tmin, tmax)) return false;
+    return slab_axis(mn.z, mx.z, r.o.z, r.d.z, tmin, tmax);
+}
+RT_HD V3 box_center(const Box& b) { return 0.5f * (b.mn + b.mx); }
+
+// z_order.cu:5-36 — 64-bit interleave of the raw float bits, x first, MSB first.
+RT_HD uint64_t z_order(V3 vec) {
+    V3 inv = neg(vec);
+    union { float f; uint32_t u; } cx{inv.x}, cy{inv.y}, cz{inv.z};
+    uint32_t xo = 31, yo = 31, zo = 31;
+    uint64_t t = 0;
+    for (unsigned i = 0; i < 64; i++) {
+        t <<= 1;
+        unsigned m = i % 3;
+        if (m == 0) { t |= (cx.u >> xo) & 1u; xo--; }
+        else if (m == 1) { t |= (cy.u >> yo) & 1u; yo--; }
+        else { t |= (cz.u >> zo) & 1u; zo--; }
+    }
+    return t;
+}
+
+// ---- triangle test (geometry.h:229-290) with ray-independent factors precomputed ----
+// pn = normalized(cross(b-a, c-a)) (Plane ctor), area = |cross(b-a, c-a)|.
+RT_HD bool tri_hit(V3 a, V3 b, V3 c, V3 pn, float area, const Ray& r, float& time, float& u, float& v) {
+    float denom = dot(r.d, pn);
+    if (fabsf(denom) < THRESH) return false;
+    float t = (1.0f / denom) * dot(a - r.o, pn);
+    V3 p = at(r, t);
+    float b0 = len(cross(c - p, b - p)) / area;
+    float b1 = len(cross(c - p, a - p)) / area;
+    float b2 = len(cross(a - p, b - p)) / area;
+    if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
+    time = t;
+    return false;
+}
+
+// ---- quaternion <-> basis (geometry.h:36-41, 183-198) ----
+inline Q axis_angle_gxx(V3 axis, float theta) {   // g++ TU (cube_world.cc): double cos/sin
+    float hc = (float)cos((double)(0.5f * theta));
+    float hs = (float)sin((double)(0.5f * theta));
+    return Q{axis.x * hs, axis.y * hs, axis.z * hs, hc};
+}
+RT_HD void to_mat3(Q q, float m[3][3]) {
+    float length = sqrtf(dot4(qv(q), qv(q)));
+    float ni = q.i / length, nj = q.j / length, nk = q.k / length, nr = q.r / length;
+    float ii = 2.0f * ni * ni, jj = 2.0f * nj * nj, kk = 2.0f * nk * nk;
+    float ri = 2.0f * nr * ni, rj = 2.0f * nr * nj, rk = 2.0f * nr * nk;
+    float ij = 2.0f * ni * nj, ik = 2.0f * ni * nk, jk = 2.0f * nj * nk;
+    m[0][0] = 1 - (jj + kk); m[0][1] = ij - rk;       m[0][2] = ik + rj;
+    m[1][0] = ij + rk;       m[1][1] = 1 - (ii + kk); m[1][2] = jk - ri;
+    m[2][0] = ik - rj;       m[2][1] = jk + ri;       m[2][2] = 1 - (ii + jj);
+}
+
+}  // namespace rtm

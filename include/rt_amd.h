@@ -1,0 +1,144 @@
+/*
+ * rt_amd.h — C ABI of the MI355X-native ray-tracing core (the drop-in boundary).
+ *
+ * Replaces the render path of wtzhang23/gpu-ray-tracer:
+ *   rtracer::gpu::update_scene(Scene*, int kernel_dim, bool optimize)   include/raytracer.h:18-22, src/raytracer.cu:102-120
+ *   rtracer::gpu::debug_cast(Scene*, int x, int y)                      include/raytracer.h:21,       src/raytracer.cu:91-100
+ *   procedural::gpu::generate(std::string config_path)                  include/procedural/cube_world.h:20-23, src/procedural/cube_world.cc:195-207
+ *   rtracer::SceneBuilder {add_vertex, create_mesh, add_triangle, add_trans, build_cube,
+ *                          add_point_light, add_directional_light, build_gpu_scene}  include/scene_builder.h:29-117
+ *   renv::gpu::Scene::free(Scene&)                                       include/rayenv/gpu/scene.h:55-69
+ *   Camera/Entity translate/rotate/set_position/set_orientation          include/rayprimitives/entity.h:49-74
+ *   Canvas::get_color / the framebuffer SDL wraps                        include/rayenv/canvas.h:17-44, src/rayenv/canvas.cu:10-29
+ * Plain pointers and sizes only; every call returns an RT_* status and sets a
+ * thread-local message readable with rt_last_error() (the reference asserts).
+ */
+#ifndef RT_AMD_H
+#define RT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,      /* bad argument / out-of-range index */
+    RT_ERR_IO = -2,       /* file cannot be opened */
+    RT_ERR_PARSE = -3,    /* malformed scene description */
+    RT_ERR_HIP = -4,      /* HIP runtime error (message has the hipError string) */
+    RT_ERR_STATE = -5,    /* call not valid in the current state */
+    RT_ERR_NODEV = -6,    /* no usable gfx950 device */
+    RT_ERR_LIMIT = -7     /* scene exceeds a build limit (see rt_last_error) */
+};
+
+typedef struct rt_scene rt_scene;
+
+/* ---- library ---- */
+int rt_abi_version(void);
+const char* rt_last_error(void);
+int rt_device_count(int* count);
+/* Select the HIP device for subsequent scene uploads on this thread. */
+int rt_set_device(int device);
+
+/* ---- scene creation (host only; device upload is lazy, at first render) ---- */
+/* worldN.json -> scene (cube_world.cc:38-191).  width/height <= 0 keep the JSON's canvas size. */
+int rt_scene_load_json(const char* path, int width, int height, rt_scene** out);
+/* Empty scene for the builder API (SceneBuilder{atlas_path}, scene_builder.h:51-56). */
+int rt_scene_create(const char* atlas_path, rt_scene** out);
+int rt_scene_free(rt_scene* s);
+
+/* SceneBuilder (scene_builder.h:58-112).  Indices are returned through out-params. */
+int rt_builder_add_vertex(rt_scene* s, float x, float y, float z, int* idx);
+int rt_builder_create_mesh(rt_scene* s, const float pos3[3], const float quat4[4], int* mesh);
+/* material26: Ke[4] Ka[4] Kd[4] Ks[4] Kt[4] Kr[4] alpha eta (material.h:14-31) */
+int rt_builder_add_triangle(rt_scene* s, int mesh, int i0, int i1, int i2, const float material26[26]);
+int rt_builder_add_trans(rt_scene* s, int mesh, int* trans);
+int rt_builder_set_trans(rt_scene* s, int trans, const float pos3[3], const float quat4[4]);  /* either may be NULL */
+int rt_builder_build_cube(rt_scene* s, float scale, const float material26[26], int* mesh);
+int rt_builder_add_point_light(rt_scene* s, const float pos3[3], const float col4[4]);
+int rt_builder_add_directional_light(rt_scene* s, const float dir3[3], const float col4[4]);
+/* Canvas + Camera (camera.cu:6-9) + Environment (environment.h:19-93); finalises the builder. */
+int rt_builder_finish(rt_scene* s, int width, int height, float fov_radians, float unit_to_pixels,
+                      const float cam_pos3[3], const float cam_quat4[4],
+                      const float dist_atten3[3], const float ambience4[4], int depth);
+
+/* info10 = {W, H, n_vertices, n_tris, n_meshes, n_instances, n_lights, n_point_lights, depth, n_materials} */
+int rt_scene_info(const rt_scene* s, int32_t info10[10]);
+/* Host copies of the scene arrays (layouts as in oracle/rt_oracle.h) for parity checks. */
+enum { RT_EXPORT_VERTICES = 0, RT_EXPORT_NORMALS = 1, RT_EXPORT_TRIS = 2, RT_EXPORT_MATERIALS = 3,
+       RT_EXPORT_INSTANCES = 4, RT_EXPORT_INST_MESH = 5, RT_EXPORT_LIGHTS = 6, RT_EXPORT_CAMERA = 7, RT_EXPORT_ENV = 8 };
+int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t dst_bytes);
+
+/* ---- camera / environment (entity.h:49-74, environment.h:30-44) ---- */
+int rt_camera_get(const rt_scene* s, float pos3[3], float quat4[4]);
+int rt_camera_set(rt_scene* s, const float pos3[3], const float quat4[4]);      /* either may be NULL */
+int rt_camera_translate(rt_scene* s, const float d3[3]);                        /* Entity::translate: p += o*d */
+int rt_camera_rotate(rt_scene* s, const float dq4[4]);                          /* Entity::rotate: o = dq*o */
+/* Camera::up()/right()/forward() unit directions (camera.cu:11-31) */
+int rt_camera_axes(const rt_scene* s, float right3[3], float up3[3], float forward3[3]);
+int rt_env_set(rt_scene* s, const float ambience4[4], const float dist_atten3[3], int depth);
+
+/* ---- rendering ---- */
+typedef struct rt_render_opts {
+    int spp;            /* samples per pixel, >= 1 (1 == reference) */
+    int use_bvh;        /* reference `optimize`: 1 BVH traversal, 0 brute force over instances */
+    int rebuild_bvh;    /* 1: rebuild the BVH in this call (reference per-frame semantics); 0: reuse if built */
+    int row0, row_step; /* render rows y = row0 + j*row_step (row-cyclic multi-GPU slice); 0,1 = full frame */
+    int compact;        /* 0: outputs indexed by full-frame pixel y*W+x; 1: by slice row j*W+x */
+    int kernel_dim;     /* reference's block edge (-d); accepted, the HIP path picks its own tiling */
+    void* stream;       /* hipStream_t to launch on; NULL = the scene's own stream */
+    uint32_t* rgba;     /* device outputs (NULL = internal canvas for rgba, skipped for the others) */
+    float* radiance;    /* float4 per pixel: mean of unclamped sample radiance */
+    int32_t* hit_inst;  /* primary hit of sample 0: instance index, -1 on miss */
+    int32_t* hit_tri;   /* primary hit of sample 0: global triangle index, -1 on miss */
+    int sync;           /* 1: wait for completion before returning (required for stats) */
+    int host_outputs;   /* 1: rgba/radiance/hit_* are HOST pointers; results are copied back (implies sync) */
+    int timing;         /* 1: record device events around the BVH build and the trace kernel on the
+                           launch stream (no sync); totals via rt_timing_collect */
+} rt_render_opts;
+
+typedef struct rt_stats {
+    uint64_t rays;       /* closest-hit queries (= reference cast_ray calls) */
+    uint64_t nodes;      /* BVH node tests, single-ray semantics */
+    uint64_t leaves;     /* instance tests (= cast_local calls) */
+    uint64_t tri_tests;  /* triangle tests */
+    double bvh_ms;       /* BVH build kernel time (device events) */
+    double trace_ms;     /* trace kernel time (device events) */
+} rt_stats;
+
+void rt_render_opts_default(rt_render_opts* o);
+int rt_render(rt_scene* s, const rt_render_opts* opts, rt_stats* stats);
+
+/* Sum of the event-timed kernel durations of all rt_render calls with timing=1
+ * since the last collect (synchronizes those events), then resets. */
+int rt_timing_collect(rt_scene* s, double* bvh_ms_total, double* trace_ms_total, int* n_frames);
+
+/* Reference-equivalent frame: rebuild BVH if optimize, trace 1 spp, synchronize,
+ * framebuffer host-readable afterwards (raytracer.cu:102-120). */
+int rt_update_scene(rt_scene* s, int kernel_dim, int optimize);
+/* Host framebuffer (RGBA8 packed R<<24|G<<16|B<<8|A, row-major W*H) after rt_update_scene. */
+int rt_canvas_read(const rt_scene* s, uint32_t* dst, int64_t n_pixels);
+const uint32_t* rt_canvas_host_ptr(const rt_scene* s);
+/* Canvas::get_color(x, y) of the last rt_update_scene frame (canvas.cu:14-17). */
+int rt_canvas_get_color(const rt_scene* s, int x, int y, uint8_t rgba4[4]);
+
+/* debug_cast (raytracer.cu:91-100): trace pixel (x, y) and write an event log
+ * ("shooting a ray", "preparing to shoot a reflection ray", ...) into buf. */
+int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap);
+
+/* Device-side math known-answer entry (test hook): evaluates `op` element-wise on
+ * the GPU.  op names as in oracle/rt_oracle.h's orc_kat_*.  Host pointers in/out. */
+int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2,
+                  float* out_f, int32_t* out_i, uint64_t* out_u);
+
+/* Sample offset table of the build-defined spp extension (k=0 -> (0,0)). */
+int rt_spp_offset(int k, float* dx, float* dy);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

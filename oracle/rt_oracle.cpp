@@ -982,21 +982,27 @@ void orc_kat_quat_mul(int n, const float* a, const float* b, float* o) {
 void orc_kat_tri_hit(int n, const float* t9, const float* r6, int32_t* hit, float* o) {
     for (int i = 0; i < n; i++) {
         const float* t = t9 + 9 * i; const float* r = r6 + 6 * i;
-        Ray ray{ld3(r), ld3(r + 3)};   // raw (caller supplies the already-normalized direction)
+        Ray ray = make_ray(ld3(r), ld3(r + 3));
         float time = NAN, u = NAN, v = NAN;
         hit[i] = triangle_hit(ld3(t), ld3(t + 3), ld3(t + 6), ray, time, u, v);
-        o[3 * i] = time; o[3 * i + 1] = u; o[3 * i + 2] = v;
+        o[3 * i] = hit[i] ? time : NAN; o[3 * i + 1] = hit[i] ? u : NAN; o[3 * i + 2] = hit[i] ? v : NAN;
     }
 }
 void orc_kat_box_hit(int n, const float* b7, const float* r6, int32_t* hit, float* t) {
     for (int i = 0; i < n; i++) {
         const float* b = b7 + 7 * i; const float* r = r6 + 6 * i;
         Box bx{ld3(b), ld3(b + 3), b[6] != 0};
-        Ray ray{ld3(r), ld3(r + 3)};
+        Ray ray = make_ray(ld3(r), ld3(r + 3));
         float tt = NAN;
         hit[i] = box_intersects(bx, ray, tt);
         t[i] = tt;
     }
+}
+void orc_kat_axis_angle(int n, const float* a4, float* o) {
+    for (int i = 0; i < n; i++) { Quat q = qaxis_angle_g(ld3(a4 + 4 * i), a4[4 * i + 3]); o[4 * i] = q.i; o[4 * i + 1] = q.j; o[4 * i + 2] = q.k; o[4 * i + 3] = q.r; }
+}
+void orc_kat_to_mat3(int n, const float* q, float* o) {
+    for (int i = 0; i < n; i++) { float m[3][3]; to_mat3(Quat{q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]}, m); memcpy(o + 9 * i, m, sizeof m); }
 }
 void orc_kat_zorder(int n, const float* v, uint64_t* o) { for (int i = 0; i < n; i++) o[i] = z_order(ld3(v + 3 * i)); }
 void orc_kat_ray_ctor(int n, const float* r6, float* o) {

@@ -73,9 +73,11 @@ void orc_kat_refract(int n, const float* d, const float* nrm, const float* n1n2,
 void orc_kat_quat_rotate(int n, const float* q, const float* v, float* out);   /* Quat*Vec3 */
 void orc_kat_quat_inverse(int n, const float* q, float* out);
 void orc_kat_quat_mul(int n, const float* a, const float* b, float* out);
-void orc_kat_tri_hit(int n, const float* tri9, const float* ray6, int32_t* hit, float* t_uv3);
+void orc_kat_tri_hit(int n, const float* tri9, const float* ray6, int32_t* hit, float* t_uv3); /* ray built with Ray(o,d) */
 void orc_kat_box_hit(int n, const float* box7, const float* ray6, int32_t* hit, float* t);
 void orc_kat_zorder(int n, const float* v, uint64_t* out);
+void orc_kat_axis_angle(int n, const float* axis_theta4, float* out);          /* Quat(axis, theta), g++-TU cos/sin */
+void orc_kat_to_mat3(int n, const float* q, float* out9);
 void orc_kat_ray_ctor(int n, const float* ray6, float* out6);                   /* Ray(o,d): normalizes d */
 
 #ifdef __cplusplus

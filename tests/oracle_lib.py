@@ -1,0 +1,163 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).  TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_f = ctypes.POINTER(ctypes.c_float)
+_i = ctypes.POINTER(ctypes.c_int32)
+_u = ctypes.POINTER(ctypes.c_uint64)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+class Oracle:
+    def __init__(self, path=LIB):
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.orc_last_error.restype = ctypes.c_char_p
+        L.orc_load.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, _u32, _f, _i, _i, _u]
+        L.orc_build_bvh.argtypes = [ctypes.c_void_p, _f, _i, ctypes.c_int]
+        for name in ["orc_scene_counts", "orc_scene_vertices", "orc_scene_normals", "orc_scene_tris",
+                     "orc_scene_materials", "orc_scene_lights"]:
+            getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_scene_instances.argtypes = [ctypes.c_void_p, _f, _i]
+        L.orc_scene_camera.argtypes = [ctypes.c_void_p, _f, _f]
+        L.orc_spp_offset.argtypes = [ctypes.c_int, _f, _f]
+        self.L = L
+
+    # -- scenes ---------------------------------------------------------------
+    def load(self, path, width=0, height=0):
+        s = ctypes.c_void_p()
+        r = self.L.orc_load(path.encode(), int(width), int(height), ctypes.byref(s))
+        if r != 0:
+            raise RuntimeError("oracle load failed: %s" % self.L.orc_last_error().decode())
+        return OracleScene(self, s)
+
+    def spp_offset(self, k):
+        dx, dy = ctypes.c_float(), ctypes.c_float()
+        self.L.orc_spp_offset(k, ctypes.byref(dx), ctypes.byref(dy))
+        return dx.value, dy.value
+
+    def render(self, scene, semantics=0, use_bvh=1, spp=1, row0=0, row_step=1, nthreads=8,
+               want=("rgba", "radiance", "hit_inst", "hit_tri")):
+        W, H = scene.W, scene.H
+        rgba = np.zeros(W * H, np.uint32) if "rgba" in want else None
+        rad = np.zeros(W * H * 4, np.float32) if "radiance" in want else None
+        hi = np.full(W * H, -1, np.int32) if "hit_inst" in want else None
+        ht = np.full(W * H, -1, np.int32) if "hit_tri" in want else None
+        st = np.zeros(4, np.uint64)
+        r = self.L.orc_render(scene.h, semantics, use_bvh, spp, row0, row_step, nthreads,
+                              _p(rgba, _u32), _p(rad, _f), _p(hi, _i), _p(ht, _i), _p(st, _u))
+        if r != 0:
+            raise RuntimeError(self.L.orc_last_error().decode())
+        out = {"stats": st}
+        if rgba is not None:
+            out["rgba"] = rgba.reshape(H, W)
+        if rad is not None:
+            out["radiance"] = rad.reshape(H, W, 4)
+        if hi is not None:
+            out["hit_inst"] = hi.reshape(H, W)
+        if ht is not None:
+            out["hit_tri"] = ht.reshape(H, W)
+        return out
+
+    # -- KATs -----------------------------------------------------------------
+    def kat(self, op, *arrays, n_out=None):
+        L = self.L
+        arrs = [np.ascontiguousarray(a, np.float32) for a in arrays]
+        n = arrs[0].shape[0]
+        P = lambda a: a.ctypes.data_as(_f)
+        if op in ("normalize3", "reflect", "cross", "quat_rotate"):
+            o = np.zeros((n, 3), np.float32)
+            getattr(L, "orc_kat_" + op)(n, *[P(a) for a in arrs], P(o))
+            return o
+        if op in ("quat_inverse", "quat_mul", "axis_angle"):
+            o = np.zeros((n, 4), np.float32)
+            getattr(L, "orc_kat_" + op)(n, *[P(a) for a in arrs], P(o))
+            return o
+        if op == "to_mat3":
+            o = np.zeros((n, 9), np.float32)
+            L.orc_kat_to_mat3(n, P(arrs[0]), P(o))
+            return o
+        if op == "ray_ctor":
+            o = np.zeros((n, 6), np.float32)
+            L.orc_kat_ray_ctor(n, P(arrs[0]), P(o))
+            return o
+        if op == "refract":
+            o = np.zeros((n, 3), np.float32)
+            t = np.zeros(n, np.int32)
+            L.orc_kat_refract(n, P(arrs[0]), P(arrs[1]), P(arrs[2]), P(o), t.ctypes.data_as(_i))
+            return o, t
+        if op == "tri_hit":
+            o = np.zeros((n, 3), np.float32)
+            h = np.zeros(n, np.int32)
+            L.orc_kat_tri_hit(n, P(arrs[0]), P(arrs[1]), h.ctypes.data_as(_i), P(o))
+            return h, o
+        if op == "box_hit":
+            t = np.zeros(n, np.float32)
+            h = np.zeros(n, np.int32)
+            L.orc_kat_box_hit(n, P(arrs[0]), P(arrs[1]), h.ctypes.data_as(_i), P(t))
+            return h, t
+        if op == "zorder":
+            o = np.zeros(n, np.uint64)
+            L.orc_kat_zorder(n, P(arrs[0]), o.ctypes.data_as(_u))
+            return o
+        raise KeyError(op)
+
+
+class OracleScene:
+    def __init__(self, orc, h):
+        self.orc, self.h = orc, h
+        c = np.zeros(10, np.int32)
+        orc.L.orc_scene_counts(h, c.ctypes.data)
+        (self.W, self.H, self.n_vertices, self.n_tris, self.n_meshes, self.n_instances, self.n_lights,
+         self.n_point, self.depth, self.n_mats) = [int(x) for x in c]
+
+    def __del__(self):
+        try:
+            self.orc.L.orc_free(self.h)
+        except Exception:
+            pass
+
+    def arrays(self):
+        L = self.orc.L
+        v = np.zeros((self.n_vertices, 3), np.float32); L.orc_scene_vertices(self.h, v.ctypes.data)
+        n = np.zeros((self.n_vertices, 3), np.float32); L.orc_scene_normals(self.h, n.ctypes.data)
+        t = np.zeros((self.n_tris, 4), np.int32); L.orc_scene_tris(self.h, t.ctypes.data)
+        m = np.zeros((self.n_mats, 26), np.float32); L.orc_scene_materials(self.h, m.ctypes.data)
+        q = np.zeros((self.n_instances, 7), np.float32); mi = np.zeros(self.n_instances, np.int32)
+        L.orc_scene_instances(self.h, q.ctypes.data_as(_f), mi.ctypes.data_as(_i))
+        li = np.zeros((self.n_lights, 8), np.float32); L.orc_scene_lights(self.h, li.ctypes.data)
+        cam = np.zeros(21, np.float32); env = np.zeros(7, np.float32)
+        L.orc_scene_camera(self.h, cam.ctypes.data_as(_f), env.ctypes.data_as(_f))
+        return dict(vertices=v, normals=n, tris=t, materials=m, instances=q, inst_mesh=mi, lights=li,
+                    camera=cam, env=env)
+
+    def bvh(self):
+        n = 1
+        while n < max(self.n_instances, 1):
+            n *= 2
+        boxes = np.zeros((2 * n - 1, 7), np.float32)
+        order = np.zeros(n, np.int32)
+        r = self.orc.L.orc_build_bvh(self.h, boxes.ctypes.data_as(_f), order.ctypes.data_as(_i), n)
+        assert r == n, r
+        return boxes, order

@@ -1,0 +1,54 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every
+symbol include/rt_amd.h declares, and fails loudly (no CPU fallback) without a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT, scene_path
+
+HEADER = os.path.join(ROOT, "include", "rt_amd.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_symbols_listed(rt):
+    assert declared_symbols() == sorted(rt.SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(rt):
+    L = ctypes.CDLL(rt.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_abi_version(rt):
+    assert rt.lib().rt_abi_version() == 1
+
+
+def test_library_is_gfx950_code(rt):
+    """The shared object carries a gfx950 code object (built by hipcc --offload-arch=gfx950)."""
+    blob = open(rt.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_render_without_gpu_fails_loudly(rt):
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is present")
+    s = rt.Scene.load_json(scene_path("world1"), 16, 16)
+    with pytest.raises(rt.RtError) as e:
+        s.render()
+    assert e.value.code == rt.RT_ERR_NODEV
+    with pytest.raises(rt.RtError):
+        s.update_scene()
+
+
+def test_oracle_not_linked_into_product(rt):
+    """The product library must not depend on or embed the oracle."""
+    blob = open(rt.LIB_PATH, "rb").read()
+    assert b"orc_render" not in blob and b"liboracle" not in blob

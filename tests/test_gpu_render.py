@@ -1,0 +1,127 @@
+"""GPU parity tests of the hot path: full frames from the HIP trace kernel (through
+the C ABI) against the oracle on the same scenes.
+
+Bar (BASELINE north_star): primary hit indices (instance, triangle) identical
+pixel-for-pixel; radiance within 1e-5 relative; counters (rays / BVH nodes /
+leaves / triangle tests) identical; RGBA8 identical except where a 1-ulp
+radiance difference crosses a byte boundary (pow is not bit-reproducible,
+DESIGN.md §Exactness) — such bytes may differ by exactly 1.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, scene_path
+
+pytestmark = pytest.mark.gpu
+
+RAD_RTOL = 1e-5
+
+
+def check_frame(gpu_fr, orc_fr, spp=1):
+    assert np.array_equal(gpu_fr["hit_inst"], orc_fr["hit_inst"])
+    assert np.array_equal(gpu_fr["hit_tri"], orc_fr["hit_tri"])
+    a, b = gpu_fr["radiance"].astype(np.float64), orc_fr["radiance"].astype(np.float64)
+    err = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
+    err[(a == b)] = 0
+    assert err.max() <= RAD_RTOL, float(err.max())
+    ga = gpu_fr["rgba"].view(np.uint8).astype(int)
+    oa = orc_fr["rgba"].view(np.uint8).astype(int)
+    d = np.abs(ga - oa)
+    assert d.max() <= 1, int(d.max())
+    frac = (d > 0).mean()
+    assert frac < 1e-3, frac
+    return int((d > 0).sum())
+
+
+@pytest.mark.parametrize("scene,w,h,bvh,spp", [
+    ("world1", 256, 256, 1, 1),
+    ("world1", 320, 240, 0, 1),          # brute force (config 2 mode)
+    ("world8", 320, 240, 1, 1),
+    ("world8_stress", 320, 240, 1, 1),
+    ("world8_stress", 160, 120, 1, 8),
+    ("world16", 256, 192, 1, 1),
+    ("config", 200, 150, 1, 2),
+])
+def test_frame_parity(gpu, oracle, scene, w, h, bvh, spp):
+    s = gpu.Scene.load_json(scene_path(scene), w, h)
+    fr = s.render(spp=spp, use_bvh=bool(bvh), want=("rgba", "radiance", "hit_inst", "hit_tri"))
+    o = oracle.render(oracle.load(scene_path(scene), w, h), use_bvh=bvh, spp=spp, nthreads=8)
+    check_frame(fr, o, spp)
+    st = fr["stats"]
+    assert (st["rays"], st["nodes"], st["leaves"], st["tri_tests"]) == tuple(int(x) for x in o["stats"])
+
+
+def test_golden_fixture_frames(gpu):
+    """The committed oracle frames (GPU semantics) reproduce on the device."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "frame_*_gpu.npz"))):
+        name = os.path.basename(f)[len("frame_"):-4].split("_")
+        spp, bvh = int(name[-2][3:]), name[-3] == "bvh"
+        w, h = map(int, name[-4].split("x"))
+        scene = "_".join(name[:-4])
+        g = np.load(f)
+        s = gpu.Scene.load_json(scene_path(scene), w, h)
+        fr = s.render(spp=spp, use_bvh=bvh, want=("rgba", "radiance", "hit_inst", "hit_tri"))
+        check_frame(fr, {k: g[k] for k in ("rgba", "radiance", "hit_inst", "hit_tri")}, spp)
+
+
+def test_update_scene_postcondition(gpu, oracle):
+    """rt_update_scene == rtracer::gpu::update_scene: frame complete and host-readable on return."""
+    s = gpu.Scene.load_json(scene_path("world8"), 200, 120)
+    s.update_scene(kernel_dim=16, optimize=True)
+    c = s.canvas()
+    o = oracle.render(oracle.load(scene_path("world8"), 200, 120), spp=1, nthreads=8, want=("rgba",))
+    assert np.array_equal(c, o["rgba"])
+    y, x = 60, 100
+    v = int(c[y, x])
+    assert s.get_color(x, y) == ((v >> 24) & 255, (v >> 16) & 255, (v >> 8) & 255, v & 255)
+    s.update_scene(kernel_dim=8, optimize=False)          # brute force gives the same image
+    assert np.array_equal(s.canvas(), c)
+
+
+def test_row_slices_compose(gpu):
+    """Row-cyclic slices (multi-GPU partition) rendered separately equal the full frame."""
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 96)
+    full = s.render(spp=2, want=("rgba", "hit_inst"))
+    G = 3
+    out = np.zeros_like(full["rgba"])
+    for r in range(G):
+        part = s.render(spp=2, row0=r, row_step=G, compact=True, want=("rgba",))
+        out[r::G] = part["rgba"]
+    assert np.array_equal(out, full["rgba"])
+
+
+def test_camera_move_rerender(gpu, oracle):
+    """Interactive camera (main.cc:140-180): after translate/rotate the frame still matches the oracle
+    rendering of the same camera pose."""
+    s = gpu.Scene.load_json(scene_path("world8"), 128, 96)
+    s.translate_camera([0.5, -2.0, 1.0])
+    import math
+    a = 0.05
+    s.rotate_camera([math.sin(a / 2), 0, 0, math.cos(a / 2)])
+    fr = s.render(want=("rgba", "hit_inst"))
+    # The oracle has no camera setter: compare against the reference semantics through
+    # invariants instead — the image changed and it is still a valid render.
+    s2 = gpu.Scene.load_json(scene_path("world8"), 128, 96)
+    assert not np.array_equal(fr["rgba"], s2.render()["rgba"])
+    assert (fr["hit_inst"] >= -1).all() and fr["hit_inst"].max() < s.info()["n_instances"]
+
+
+def test_debug_cast_log(gpu):
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 320, 240)
+    fr = s.render(want=("hit_inst",))
+    ys, xs = np.nonzero(fr["hit_inst"] >= 0)
+    log = s.debug_cast(int(xs[0]), int(ys[0]))
+    assert log[0] == "shooting a ray" and "shooting shadow ray" in log
+    ys, xs = np.nonzero(fr["hit_inst"] < 0)
+    assert s.debug_cast(int(xs[0]), int(ys[0])) == ["shooting a ray"]
+
+
+def test_empty_scene_renders_black(gpu, tmp_path):
+    p = tmp_path / "empty.json"
+    p.write_text('{"atlas": "x", "grid_size": 0, "cubes": [], "width": 40, "height": 30}')
+    s = gpu.Scene.load_json(str(p))
+    fr = s.render(want=("rgba", "hit_inst"))
+    assert (fr["rgba"] == 0).all() and (fr["hit_inst"] == -1).all()
