@@ -64,7 +64,7 @@ struct Hit {                 // rprimitives::Isect (isect.h:15-24) minus texture
     int mat, inst, tri;
 };
 
-struct Counters { unsigned long long rays, nodes, leaves, tris; };
+struct Counters { unsigned rays, nodes, leaves, tris; };   // per lane per frame
 
 struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DTri* __restrict__ tris;
@@ -76,15 +76,49 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     int n_leaf, n_inst, n_lights, use_bvh;
 };
 
+// Wave-uniform read-only records are read through the constant address space so
+// that uniform indices compile to scalar (SMEM) loads.
+template <class T> __device__ __forceinline__ T ldc(const T* p, int i) {
+    static_assert(sizeof(T) % 4 == 0, "4-byte granular records");
+    T r;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __attribute__((address_space(4))) uint32_t* s = (const __attribute__((address_space(4))) uint32_t*)(p + i);
+#else
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(p + i);
+#endif
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(T) / 4); w++) d[w] = s[w];
+    return r;
+}
+
+// Triangle test of Triangle::hit (geometry.h:273-290) fused with TriInner::tri_hit's
+// acceptance (trimesh.cu:56: time >= 1e-5 && time < isect.time).  The acceptance
+// bound is checked right after the plane intersection — before the barycentric
+// lengths — which changes nothing observable: a rejected triangle has no effect.
+__device__ __forceinline__ bool tri_accept(const DTri& T, const Ray& r, float best, float& time, float& u, float& v) {
+    float denom = dot(r.d, T.pn);
+    if (fabsf(denom) < THRESH) return false;
+    float t = (1.0f / denom) * dot(T.a - r.o, T.pn);
+    if (!(t >= THRESH && t < best)) return false;
+    V3 p = at(r, t);
+    float b0 = len(cross(T.c - p, T.b - p)) / T.area;
+    float b1 = len(cross(T.c - p, T.a - p)) / T.area;
+    float b2 = len(cross(T.a - p, T.b - p)) / T.area;
+    if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
+    return false;
+}
+
 // ---------------------------------------------------------------------------
 // Closest hit against one instance: renv::gpu::cast_local (scene.cu:27-40) ->
 // Hitable::hit (hitable.cu:29-38) -> Trimesh::hit_local (trimesh.cu:11-19).
 // `ti` is wave-uniform; the lane's own ray is tested against every triangle of
-// the mesh in index order, accepting t >= 1e-5 && t < h.time (trimesh.cu:56).
+// the mesh in index order.  The interpolated normal is only formed for the last
+// accepted triangle (earlier ones are overwritten in the reference too).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool cast_local(const SceneView& S, int ti, const Ray& r, Hit& h, Counters& c) {
-    const DInst inst = S.insts[ti];
-    const DMesh mesh = S.meshes[inst.mesh];
+    const DInst inst = ldc(S.insts, ti);
+    const DMesh mesh = ldc(S.meshes, inst.mesh);
     c.leaves++;
     V3 ld = vec_to_local(inst.pose, r.d);
     float dir_len = len(ld);
@@ -95,22 +129,19 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, int ti, const Ray
     int best = -1;
     float bu = 0.0f, bv = 0.0f;
     const int t0 = mesh.tri_begin, t1 = mesh.tri_begin + mesh.tri_count;
-    c.tris += (unsigned long long)mesh.tri_count;
+    c.tris += (unsigned)mesh.tri_count;
     for (int t = t0; t < t1; t++) {
-        const DTri& T = S.tris[t];
+        const DTri T = ldc(S.tris, t);
         float time, u, v;
-        if (tri_hit(T.a, T.b, T.c, T.pn, T.area, mr, time, u, v) && time >= THRESH && time < h.time) {
-            h.time = time; best = t; bu = u; bv = v;
-        }
+        if (tri_accept(T, mr, h.time, time, u, v)) { h.time = time; best = t; bu = u; bv = v; }
     }
     if (best < 0) return false;
-    // interpolated normal of the last accepted triangle (trimesh.cu:58-65)
-    const DTri& T = S.tris[best];
+    const DTri T = S.tris[best];                              // per-lane triangle: vector load
     float b0 = 1.0f - bu - bv;
-    V3 n = normalized((b0 * T.n0 + bu * T.n1) + bv * T.n2);
-    n = normalized(vec_from_local(mesh.pose, n));            // HitHandle::fix_isect
+    V3 n = normalized((b0 * T.n0 + bu * T.n1) + bv * T.n2);   // trimesh.cu:58-65
+    n = normalized(vec_from_local(mesh.pose, n));             // HitHandle::fix_isect
     h.time *= scale;
-    h.norm = vec_from_local(inst.pose, n);                   // cast_local
+    h.norm = vec_from_local(inst.pose, n);                    // cast_local
     h.time *= dir_len;
     h.mat = T.mat; h.inst = ti; h.tri = best;
     return true;
@@ -127,19 +158,19 @@ __device__ __forceinline__ bool cast_ray(const SceneView& S, bool active, const 
         return hit;
     }
     const int n = S.n_leaf;
-    if (active) c.nodes++;                                   // root test
+    if (active) c.nodes++;                                    // root test
     int k = 1;
     for (;;) {
-        const DNode nd = S.nodes[k];                          // wave-uniform node -> scalar loads
+        const DNode nd = ldc(S.nodes, k);                     // wave-uniform node -> scalar loads
         bool hb = active && nd.nd &&
                   box_hit(v3(nd.mnx, nd.mny, nd.mnz), v3(nd.mxx, nd.mxy, nd.mxz), r);
         if (k >= n) {                                         // leaf (at_child: 2k >= 2n-1)
             if (hb && cast_local(S, nd.inst, r, h, c)) hit = true;
         } else {
-            if (hb) c.nodes += 2;                              // single-ray DFS tests both children
-            if (__ballot(hb)) { k = 2 * k; continue; }          // step_next (bvh.cu:132-140)
+            if (hb) c.nodes += 2;                             // single-ray DFS tests both children
+            if (__ballot(hb)) { k = 2 * k; continue; }         // step_next (bvh.cu:132-140)
         }
-        while (k & 1) k >>= 1;                                // step_up (bvh.cu:116-130)
+        while (k & 1) k >>= 1;                               // step_up (bvh.cu:116-130)
         if (k == 0) break;
         k += 1;
     }
@@ -170,6 +201,7 @@ struct TraceParams {
     V3 dist_atten;
     V4 ambience;
     int W, H, row0, row_step, n_rows, compact, spp, depth;
+    int lanes_per_px, px_per_wave, gw, gh, n_gx, n_groups;   // sample-parallel lane mapping
     const float2* __restrict__ spp_off;
     uint32_t* rgba;
     float4* radiance;
@@ -195,86 +227,67 @@ __device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
     return make_ray(c.pos, dir);
 }
 
-template <int NF>
-__global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, SceneView S) {
-    // pixel of this lane: 16x16 block tile, 8x8 per wave
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int pr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);    // slice row
-    const bool valid = px < P.W && pr < P.n_rows;
-    const int py = P.row0 + pr * P.row_step;
-    const bool me = valid && px == P.dbg_x && py == P.dbg_y;
-
-    Counters cnt{0, 0, 0, 0};
-    Frame fr[NF];
-    int top = -1, k = 0, phase = valid ? 0 : PH_DONE;
-    bool primary = false;
-    V4 acc = v4(0, 0, 0, 0), sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
-    Hit is{INFINITY, v3(0, 0, 0), 0, -1, -1};                // the pixel's shared Isect
-    int hinst = -1, htri = -1;
-    // illumination state (illuminate / Light::shine / Light::attenuate)
-    int li = 0, fidx = 0;
+// One camera sample per lane through renv::gpu::propagate_ray (scene.cu:92-188),
+// run as a state machine whose only wave-collective step is the closest-hit
+// query.  The top frame lives in registers; frames suspended under a reflection
+// child (at most `depth` of them) in the private array `stk`.
+template <int NS>
+__device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, bool valid, Ray r0, bool me,
+                                           int& hinst, int& htri, Counters& cnt) {
+    Frame cur, stk[NS > 0 ? NS : 1];
+    int top = -1, phase = PH_DONE;
+    bool primary = true, pending_pop = false;
+    V4 acc = v4(0, 0, 0, 0);
+    Hit is{INFINITY, v3(0, 0, 0), 0, -1, -1};                 // the sample's shared Isect
+    int li = 0;
     V4 summed = v4(0, 0, 0, 0), rv = v4(0, 0, 0, 0);
     V3 hpos = v3(0, 0, 0), dtl = v3(0, 0, 0);
     float da = 1.0f, max_t = 0.0f;
-    Ray q{v3(0, 0, 0), v3(0, 0, 1)};
+    Ray q = r0;
+    hinst = -1; htri = -1;
 
-    // Advance the integrator until the lane needs a query or its pixel is finished.
+    auto pop = [&]() { top--; if (top >= 0) cur = stk[top]; };
     auto advance = [&]() {
         for (;;) {
-            if (top < 0) {
-                if (phase != 0) {                              // a sample just finished
-                    sum_c = sum_c + v4(acc.x > 1.0f ? 1.0f : acc.x, acc.y > 1.0f ? 1.0f : acc.y,
-                                       acc.z > 1.0f ? 1.0f : acc.z, acc.w > 1.0f ? 1.0f : acc.w);
-                    sum_r = sum_r + acc;
-                    k++;
-                }
-                if (k >= P.spp) { phase = PH_DONE; return; }
-                float2 o = P.spp_off[k];
-                Ray r = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
-                fr[0].ray = r; fr[0].hit_pt = v3(0, 0, 0); fr[0].norm = v3(0, 0, 0);
-                fr[0].atten = v4(1.0f, 1.0f, 1.0f, 1.0f); fr[0].last_mat = -1;
-                fr[0].type = F_NORMAL; fr[0].depth = P.depth; fr[0].in_obj = 0;
-                top = 0; acc = v4(0, 0, 0, 0); primary = (k == 0);
-                is.time = INFINITY;
-            }
-            Frame& f = fr[top];
-            if (f.type == F_NORMAL) {                         // scene.cu:100-128
+            if (top < 0) { phase = PH_DONE; return; }
+            if (cur.type == F_NORMAL) {                       // scene.cu:100-128
                 is.time = INFINITY;
                 dbg(P, me, 1);
-                q = f.ray; phase = PH_NORMAL; return;
+                q = cur.ray; phase = PH_NORMAL; return;
             }
             const DMat& m = S.mats[is.mat];
-            if (f.type == F_REFLECT) {                        // scene.cu:129-148
-                f.type = F_REFRACT;
+            if (cur.type == F_REFLECT) {                      // scene.cu:129-148
+                cur.type = F_REFRACT;
                 if (m.reflective) {
                     dbg(P, me, 2);
-                    Frame& c = fr[top + 1];
-                    c.type = F_NORMAL; c.last_mat = f.last_mat; c.in_obj = f.in_obj;
-                    c.atten = f.atten * m.Kr;
-                    c.depth = f.depth - 1;
-                    c.ray = make_ray(f.hit_pt, reflect(f.ray.d, normalized(f.norm)));
+                    Frame c;
+                    c.type = F_NORMAL; c.last_mat = cur.last_mat; c.in_obj = cur.in_obj;
+                    c.atten = cur.atten * m.Kr;
+                    c.depth = cur.depth - 1;
+                    c.ray = make_ray(cur.hit_pt, reflect(cur.ray.d, normalized(cur.norm)));
+                    c.hit_pt = v3(0, 0, 0); c.norm = v3(0, 0, 0);
+                    stk[top] = cur;
                     top++;
+                    cur = c;
                 }
                 continue;
             }
             // F_REFRACT (scene.cu:149-184): reads the possibly clobbered shared Isect
             if (m.refractive) {
                 dbg(P, me, 3);
-                f.type = F_NORMAL;
+                cur.type = F_NORMAL;
                 float n1, n2;
-                if (f.in_obj) { n1 = S.mats[f.last_mat].eta; n2 = 1.0f; }
-                else { n1 = 1.0f; n2 = S.mats[f.last_mat].eta; }
+                if (cur.in_obj) { n1 = S.mats[cur.last_mat].eta; n2 = 1.0f; }
+                else { n1 = 1.0f; n2 = S.mats[cur.last_mat].eta; }
                 bool tir;
-                V3 rd = refract(f.ray.d, normalized(f.norm), n1, n2, tir);
-                if (tir) top--;
-                else { f.ray = make_ray(f.hit_pt, rd); f.in_obj = !f.in_obj; f.depth--; }
+                V3 rd = refract(cur.ray.d, normalized(cur.norm), n1, n2, tir);
+                if (tir) pop();
+                else { cur.ray = make_ray(cur.hit_pt, rd); cur.in_obj = !cur.in_obj; cur.depth--; }
             } else {
-                top--;
+                pop();
             }
         }
     };
-
     // Issue the shadow query of light `li`, or finish illuminate() when all lights are done.
     auto next_light = [&]() {
         if (li < S.n_lights) {
@@ -299,19 +312,25 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, Scene
             phase = PH_SHADOW;
             return;
         }
-        acc = acc + fr[fidx].atten * summed;                   // scene.cu:127
+        acc = acc + cur.atten * summed;                         // scene.cu:127
+        if (pending_pop) { pending_pop = false; pop(); }
         advance();
     };
     auto light_done = [&](V4 att) {
         const DLight L = S.lights[li];
         V4 inc = (L.type == 0) ? da * att : att;
-        summed = summed + phong(S.mats[is.mat], is.norm, inc, fr[fidx].ray.d, dtl);
+        summed = summed + phong(S.mats[is.mat], is.norm, inc, cur.ray.d, dtl);
         li++;
         next_light();
     };
 
-    if (valid) advance();
-
+    if (valid) {
+        cur.ray = r0; cur.hit_pt = v3(0, 0, 0); cur.norm = v3(0, 0, 0);
+        cur.atten = v4(1.0f, 1.0f, 1.0f, 1.0f); cur.last_mat = -1;
+        cur.type = F_NORMAL; cur.depth = P.depth; cur.in_obj = 0;
+        top = 0;
+        advance();
+    }
     for (;;) {
         const bool need = (phase == PH_NORMAL || phase == PH_SHADOW);
         if (!__ballot(need)) break;
@@ -321,31 +340,28 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, Scene
         if (!need) continue;
         if (phase == PH_NORMAL) {
             if (primary) { primary = false; if (hit) { hinst = h.inst; htri = h.tri; } }
-            if (!hit) { is.time = INFINITY; top--; advance(); continue; }
+            if (!hit) { is.time = INFINITY; pop(); advance(); continue; }
             is.time = h.time; is.norm = h.norm; is.mat = h.mat;
-            Frame& f = fr[top];
-            fidx = top;
-            if (f.depth > 0) {                                 // scene.cu:109-121
-                if (f.in_obj) {
+            if (cur.depth > 0) {                               // scene.cu:109-121
+                if (cur.in_obj) {
                     const V4 kt = S.mats[is.mat].Kt;           // trans_atten (scene.cu:14-22): time^Kt
-                    f.atten = f.atten * v4(pow_ref(is.time, kt.x), pow_ref(is.time, kt.y),
-                                           pow_ref(is.time, kt.z), pow_ref(is.time, kt.w));
+                    cur.atten = cur.atten * v4(pow_ref(is.time, kt.x), pow_ref(is.time, kt.y),
+                                               pow_ref(is.time, kt.z), pow_ref(is.time, kt.w));
                 }
-                f.type = F_REFLECT;
-                f.hit_pt = at(f.ray, is.time);
-                f.last_mat = is.mat;
-                f.norm = is.norm;
+                cur.type = F_REFLECT;
+                cur.hit_pt = at(cur.ray, is.time);
+                cur.last_mat = is.mat;
+                cur.norm = is.norm;
             } else {
-                top--;
+                pending_pop = true;                            // popped after illumination (frame data still needed)
             }
             const DMat& m = S.mats[is.mat];                    // illuminate (phong.cu:42-53)
             summed = m.Ke + m.Ka * P.ambience;
-            hpos = at(fr[fidx].ray, is.time);
+            hpos = at(cur.ray, is.time);
             li = 0;
             next_light();
         } else {                                               // shadow segment result
-            if (!hit) { light_done(rv); continue; }
-            if (h.time > max_t) { light_done(rv); continue; }
+            if (!hit || h.time > max_t) { light_done(rv); continue; }
             const DMat& m = S.mats[h.mat];
             if (!m.refractive) { light_done(v4(0, 0, 0, 0)); continue; }
             if (dot(h.norm, q.d) > 0) {                        // calc_shadow_atten (light.cu:18-25)
@@ -357,8 +373,52 @@ __global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, Scene
             dbg(P, me, 4);
         }
     }
+    return acc;
+}
 
-    if (valid) {
+__device__ __forceinline__ V4 shfl4(V4 v, int src) {
+    return v4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+
+// One wave = one group of `px_per_wave` pixels x `lanes_per_px` samples.  Lane
+// (pixel p, sub s) traces samples k = round*L + s; the group leader sums the
+// clamped sample radiance in k order (build-defined spp extension).
+template <int NS>
+__global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, SceneView S) {
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+    const int L = P.lanes_per_px;
+    const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
+    const int gx = g % P.n_gx, gy = g / P.n_gx;
+    const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
+    const bool valid = g < P.n_groups && pix < P.px_per_wave && px < P.W && pr < P.n_rows;
+    const int py = P.row0 + pr * P.row_step;
+    const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
+    Counters cnt{0, 0, 0, 0};
+    V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
+    int hinst = -1, htri = -1;
+    const int rounds = (P.spp + L - 1) / L;
+    for (int rd = 0; rd < rounds; rd++) {
+        const int k = rd * L + sub;
+        const bool act = valid && k < P.spp;
+        Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
+        if (act) {
+            float2 o = P.spp_off[k];
+            r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
+        }
+        int hi, ht;
+        V4 c = trace_sample<NS>(P, S, act, r0, me && rd == 0, hi, ht, cnt);
+        if (rd == 0 && sub == 0) { hinst = hi; htri = ht; }
+        for (int s = 0; s < L; s++) {                          // in-order reduction over samples
+            V4 v = shfl4(c, base + s);
+            if (sub == 0 && rd * L + s < P.spp) {
+                sum_c = sum_c + v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y,
+                                   v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);   // raytracer.cu:37-40
+                sum_r = sum_r + v;
+            }
+        }
+    }
+    if (valid && sub == 0) {
         const float inv = (float)P.spp;
         const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
         // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
@@ -640,11 +700,20 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
     P.stats = s->d_stats; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
     SceneView S = view_of(s, o.use_bvh != 0);
-    dim3 grid((P.W + 15) / 16, (P.n_rows + 15) / 16);
-    const int nf = h.depth + 1;                               // frames needed: depth + 1 (<= MAX_FRAMES)
-    if (nf <= 1) hipLaunchKernelGGL(trace_kernel<1>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
-    else if (nf <= 3) hipLaunchKernelGGL(trace_kernel<3>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
-    else hipLaunchKernelGGL(trace_kernel<MAX_FRAMES>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    // sample-parallel mapping: L lanes per pixel (one sample each per round), 64/L pixels per wave
+    P.lanes_per_px = std::min(o.spp, 64);
+    P.px_per_wave = 64 / P.lanes_per_px;
+    int gw = 1;
+    if ((P.px_per_wave & (P.px_per_wave - 1)) == 0) { while (gw * gw < P.px_per_wave) gw <<= 1; }
+    else gw = P.px_per_wave;
+    P.gw = gw; P.gh = P.px_per_wave / gw;
+    P.n_gx = (P.W + P.gw - 1) / P.gw;
+    P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
+    dim3 grid((P.n_groups + (TRACE_BLOCK / 64) - 1) / (TRACE_BLOCK / 64));
+    const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
+    if (ns <= 0) hipLaunchKernelGGL(trace_kernel<0>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    else if (ns <= 2) hipLaunchKernelGGL(trace_kernel<2>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    else hipLaunchKernelGGL(trace_kernel<MAX_FRAMES - 1>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
