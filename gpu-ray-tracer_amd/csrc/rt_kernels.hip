@@ -48,7 +48,8 @@ namespace {
 
 constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
 constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
-constexpr int TRACE_BLOCK = 256;         // 16x16 pixels, 4 waves of 8x8
+constexpr int TRACE_BLOCK_P = 1024;      // persistent block: 16 waves sharing one LDS copy of the BVH
+constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -56,15 +57,9 @@ enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
 __device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b : a; }   // std::max
 // powf of the reference (nvcc pow(float,float)); evaluated in double and rounded:
 // agrees with glibc powf except for 1-ulp cases.
-__device__ __forceinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __noinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }   // rare: kept out of line
 
-struct Hit {                 // rprimitives::Isect (isect.h:15-24) minus texture data
-    float time;
-    V3 norm;
-    int mat, inst, tri;
-};
 
-struct Counters { unsigned rays, nodes, leaves, tris; };   // per lane per frame
 
 struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DTri* __restrict__ tris;
@@ -72,12 +67,15 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DInst* __restrict__ insts;
     const DMat* __restrict__ mats;
     const DLight* __restrict__ lights;
-    const DNode* __restrict__ nodes;
+    const float4* node_a;     // BVH, heap order, SoA (written by bvh_build_kernel)
+    const float2* node_b;
+    const int* leaf_inst;
+    const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
 };
 
-// Wave-uniform read-only records are read through the constant address space so
-// that uniform indices compile to scalar (SMEM) loads.
+// Wave-uniform read-only records in global memory are read through the
+// constant address space so that uniform indices compile to scalar (SMEM) loads.
 template <class T> __device__ __forceinline__ T ldc(const T* p, int i) {
     static_assert(sizeof(T) % 4 == 0, "4-byte granular records");
     T r;
@@ -109,70 +107,136 @@ __device__ __forceinline__ bool tri_accept(const DTri& T, const Ray& r, float be
     return false;
 }
 
-// ---------------------------------------------------------------------------
+// BVH node (heap index k) and instance records as the trace kernel reads them:
+// from LDS (staged once per persistent block) or, for scenes too large for LDS,
+// straight from global memory.  Degenerate boxes are stored as min=+inf, max=-inf.
+struct BvhRefs {
+    const float4* a;        // [2n] (mnx, mny, mnz, mxx)
+    const float2* b;        // [2n] (mxy, mxz)
+    const int* leaf;        // [n]  instance of leaf node n+i (bvh.cu ordering[])
+    const float4* inst;     // [n_inst] (px, py, pz, mesh | 0x80000000 if the pose is not identity)
+};
+
+__device__ __forceinline__ bool node_hit(float4 A, float2 B, const Ray& r) {
+    if (!(A.x <= A.w)) return false;                          // !nondegenerate (bounding_box.cu:63-65)
+    return box_hit(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r);
+}
+
+struct Best { float time; int inst, tri; float u, v; };     // closest accepted triangle so far
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris; };   // wave-uniform (SGPRs)
+
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
+
+__device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
+    const float4 I = bv.inst[ti];
+    const int w = __float_as_int(I.w);
+    mesh = w & 0x7fffffff;
+    if (w < 0) return ldc(S.insts, ti).pose;                  // general pose (precomputed quaternions)
+    Pose e;
+    e.p = v3(I.x, I.y, I.z); e.identity = 1;
+    return e;
+}
+
 // Closest hit against one instance: renv::gpu::cast_local (scene.cu:27-40) ->
-// Hitable::hit (hitable.cu:29-38) -> Trimesh::hit_local (trimesh.cu:11-19).
-// `ti` is wave-uniform; the lane's own ray is tested against every triangle of
-// the mesh in index order.  The interpolated normal is only formed for the last
-// accepted triangle (earlier ones are overwritten in the reference too).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool cast_local(const SceneView& S, int ti, const Ray& r, Hit& h, Counters& c) {
-    const DInst inst = ldc(S.insts, ti);
-    const DMesh mesh = ldc(S.meshes, inst.mesh);
-    c.leaves++;
-    V3 ld = vec_to_local(inst.pose, r.d);
+// Hitable::hit (hitable.cu:29-38) -> Trimesh::hit_local (trimesh.cu:11-19) with a
+// wave-uniform instance; times are rescaled here exactly as in the reference
+// (later comparisons depend on them); the normal is formed after traversal.
+__device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b) {
+    int mesh_id;
+    const Pose ip = inst_pose(S, bv, ti, mesh_id);
+    mesh_id = uni(mesh_id);
+    const DMesh mesh = ldc(S.meshes, mesh_id);
+    V3 ld = vec_to_local(ip, r.d);
     float dir_len = len(ld);
-    Ray lr = make_ray(point_to_local(inst.pose, r.o), ld);
-    V3 md = vec_to_local(mesh.pose, lr.d);                  // HitHandle::get_local_ray
+    Ray lr = make_ray(point_to_local(ip, r.o), ld);
+    V3 md = vec_to_local(mesh.pose, lr.d);                   // HitHandle::get_local_ray
     float scale = len(md);
     Ray mr = make_ray(point_to_local(mesh.pose, lr.o), md);
     int best = -1;
-    float bu = 0.0f, bv = 0.0f;
-    const int t0 = mesh.tri_begin, t1 = mesh.tri_begin + mesh.tri_count;
-    c.tris += (unsigned)mesh.tri_count;
-    for (int t = t0; t < t1; t++) {
+    float bu = 0.0f, bv_ = 0.0f, t_best = b.time;
+    for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
         const DTri T = ldc(S.tris, t);
         float time, u, v;
-        if (tri_accept(T, mr, h.time, time, u, v)) { h.time = time; best = t; bu = u; bv = v; }
+        if (tri_accept(T, mr, t_best, time, u, v)) { t_best = time; best = t; bu = u; bv_ = v; }
     }
     if (best < 0) return false;
-    const DTri T = S.tris[best];                              // per-lane triangle: vector load
-    float b0 = 1.0f - bu - bv;
-    V3 n = normalized((b0 * T.n0 + bu * T.n1) + bv * T.n2);   // trimesh.cu:58-65
-    n = normalized(vec_from_local(mesh.pose, n));             // HitHandle::fix_isect
-    h.time *= scale;
-    h.norm = vec_from_local(inst.pose, n);                    // cast_local
-    h.time *= dir_len;
-    h.mat = T.mat; h.inst = ti; h.tri = best;
+    b.time = (t_best * scale) * dir_len;                      // fix_isect, then cast_local
+    b.inst = ti; b.tri = best; b.u = bu; b.v = bv_;
     return true;
 }
 
-// renv::gpu::cast_ray (scene.cu:42-73).  Must be reached by the whole wave with
-// uniform control flow; `active` masks lanes without a pending query.
-__device__ __forceinline__ bool cast_ray(const SceneView& S, bool active, const Ray& r, Hit& h, Counters& c) {
+// World-space normal of the accepted hit (trimesh.cu:58-65, hitable.cu:20-23, scene.cu:35-37).
+__device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, const Best& b, int& mat) {
+    int mesh_id;
+    const Pose ip = inst_pose(S, bv, b.inst, mesh_id);
+    const Pose mp = S.meshes[mesh_id].pose;
+    const DTri& T = S.tris[b.tri];
+    mat = T.mat;
+    float b0 = 1.0f - b.u - b.v;
+    V3 n = normalized((b0 * T.n0 + b.u * T.n1) + b.v * T.n2);
+    n = normalized(vec_from_local(mp, n));
+    return vec_from_local(ip, n);
+}
+
+// renv::gpu::cast_ray (scene.cu:42-73) for the whole wave.  Packet traversal of
+// the reference's implicit heap: at an internal node hit by some lane, both
+// children (2k, 2k+1: adjacent records) are tested; the wave descends into 2k
+// first and keeps 2k+1 pending in a per-depth bit trail (wave-uniform, SGPR).
+// Each lane processes exactly the leaves its own ray hits, in the reference's
+// DFS order, so results equal the single-ray semantics; counters are the
+// single-ray node tests (1 + 2 per internal node hit).
+__device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active, const Ray& r,
+                                            Best& b, WaveCounters& wc) {
+    const unsigned long long am = __ballot(active);
+    wc.rays += __popcll(am);
     bool hit = false;
-    if (active) c.rays++;
-    if (!S.use_bvh || S.n_leaf == 0) {
-        for (int i = 0; i < S.n_inst; i++)
-            if (active && cast_local(S, i, r, h, c)) hit = true;
+    if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
+        for (int i = 0; i < S.n_inst; i++) {
+            wc.leaves += __popcll(am);
+            wc.tris += (unsigned long long)__popcll(am) * ldc(S.meshes, uni(__float_as_int(bv.inst[i].w) & 0x7fffffff)).tri_count;
+            if (active && cast_local(S, bv, i, r, b)) hit = true;
+        }
         return hit;
     }
     const int n = S.n_leaf;
-    if (active) c.nodes++;                                    // root test
+    wc.nodes += __popcll(am);                                  // root test
+    const bool hr = active && node_hit(bv.a[1], bv.b[1], r);
+    const unsigned long long br = __ballot(hr);
+    if (!br) return false;
+    auto leaf = [&](bool h, int li) {
+        const unsigned long long m = __ballot(h);
+        if (!m) return;
+        const int ti = uni(bv.leaf[li]);                       // leaf instance: wave-uniform
+        wc.leaves += __popcll(m);
+        wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
+        if (h && cast_local(S, bv, ti, r, b)) hit = true;
+    };
+    if (n == 1) { leaf(hr, 0); return hit; }
+    // one copy of the leaf code for both children (keeps the kernel small)
+    wc.nodes += 2ull * __popcll(br);
     int k = 1;
+    unsigned pending = 0;
     for (;;) {
-        const DNode nd = ldc(S.nodes, k);                     // wave-uniform node -> scalar loads
-        bool hb = active && nd.nd &&
-                  box_hit(v3(nd.mnx, nd.mny, nd.mnz), v3(nd.mxx, nd.mxy, nd.mxz), r);
-        if (k >= n) {                                         // leaf (at_child: 2k >= 2n-1)
-            if (hb && cast_local(S, nd.inst, r, h, c)) hit = true;
+        const int c0 = 2 * k;
+        const bool h0 = active && node_hit(bv.a[c0], bv.b[c0], r);
+        const bool h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r);
+        if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
+#pragma nounroll
+            for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : h1, c0 + c - n);
         } else {
-            if (hb) c.nodes += 2;                             // single-ray DFS tests both children
-            if (__ballot(hb)) { k = 2 * k; continue; }         // step_next (bvh.cu:132-140)
+            const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
+            wc.nodes += 2ull * (__popcll(b0) + __popcll(b1));
+            if (b0) {
+                if (b1) pending |= 1u << (31 - __clz(c0));
+                k = c0;
+                continue;
+            }
+            if (b1) { k = c0 + 1; continue; }
         }
-        while (k & 1) k >>= 1;                               // step_up (bvh.cu:116-130)
-        if (k == 0) break;
-        k += 1;
+        if (!pending) break;
+        const int d = 31 - __clz(pending);                     // deepest pending right sibling
+        pending &= ~(1u << d);
+        k = (k >> ((31 - __clz(k)) - d)) + 1;
     }
     return hit;
 }
@@ -208,6 +272,7 @@ struct TraceParams {
     int* hit_inst;
     int* hit_tri;
     unsigned long long* stats;
+    int* work;                // persistent-wave work counter (zeroed before each launch)
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
 };
@@ -228,35 +293,81 @@ __device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
 }
 
 // One camera sample per lane through renv::gpu::propagate_ray (scene.cu:92-188),
-// run as a state machine whose only wave-collective step is the closest-hit
-// query.  The top frame lives in registers; frames suspended under a reflection
-// child (at most `depth` of them) in the private array `stk`.
+// run as an explicit state machine whose only wave-collective step is the
+// closest-hit query.  Each piece of the reference's control flow appears once:
+//   ST_ADVANCE     REFLECT / REFRACT frame transitions until a NORMAL frame needs a ray
+//   ST_WAIT_NORMAL waiting for the frame's closest hit (scene.cu:101-127)
+//   ST_LIGHT       illuminate(): set up the shadow ray of light `li` (phong.cu:42-53)
+//   ST_WAIT_SHADOW waiting for a shadow segment (Light::attenuate, light.cu:29-61)
+// The top frame lives in registers; frames suspended under a reflection child (at
+// most `depth`) in the private array `stk`.  out_p >= 0: this lane carries the
+// pixel's sample 0 and records the primary hit ids there.
+enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_WAIT_SHADOW = 4 };
+
 template <int NS>
-__device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, bool valid, Ray r0, bool me,
-                                           int& hinst, int& htri, Counters& cnt) {
+__device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
+                                           Ray r0, bool me, long out_p, WaveCounters& wc) {
     Frame cur, stk[NS > 0 ? NS : 1];
-    int top = -1, phase = PH_DONE;
+    int top = -1, st = ST_DONE;
     bool primary = true, pending_pop = false;
     V4 acc = v4(0, 0, 0, 0);
-    Hit is{INFINITY, v3(0, 0, 0), 0, -1, -1};                 // the sample's shared Isect
+    float is_time = INFINITY;                                   // the sample's shared Isect
+    V3 is_norm = v3(0, 0, 0);
+    int is_mat = 0;
     int li = 0;
     V4 summed = v4(0, 0, 0, 0), rv = v4(0, 0, 0, 0);
-    V3 hpos = v3(0, 0, 0), dtl = v3(0, 0, 0);
+    V3 dtl = v3(0, 0, 0);
     float da = 1.0f, max_t = 0.0f;
     Ray q = r0;
-    hinst = -1; htri = -1;
-
-    auto pop = [&]() { top--; if (top >= 0) cur = stk[top]; };
-    auto advance = [&]() {
-        for (;;) {
-            if (top < 0) { phase = PH_DONE; return; }
-            if (cur.type == F_NORMAL) {                       // scene.cu:100-128
-                is.time = INFINITY;
-                dbg(P, me, 1);
-                q = cur.ray; phase = PH_NORMAL; return;
+    if (valid) {
+        cur.ray = r0; cur.hit_pt = v3(0, 0, 0); cur.norm = v3(0, 0, 0);
+        cur.atten = v4(1.0f, 1.0f, 1.0f, 1.0f); cur.last_mat = -1;
+        cur.type = F_NORMAL; cur.depth = P.depth; cur.in_obj = 0;
+        top = 0; st = ST_ADVANCE;
+    }
+    for (;;) {
+        // ---- local transitions until this lane waits for a query or is done ----
+        while (st == ST_ADVANCE || st == ST_LIGHT) {
+            if (st == ST_LIGHT) {
+                if (li < S.n_lights) {
+                    const DLight L = S.lights[li];
+                    const V3 hpos = at(cur.ray, is_time);          // org_ray.at(isect.time) (phong.cu:48)
+                    Ray to;
+                    if (L.type == 0) {                             // PointLight::shine (light.cu:63-70)
+                        V3 disp = L.v - hpos;
+                        float dist = len(disp);
+                        float quad = P.dist_atten.x + P.dist_atten.y * dist + P.dist_atten.z * dist * dist;
+                        da = quad < 1.0f ? 1.0f : 1.0f / quad;
+                        dtl = normalized(disp);
+                        to = make_ray(hpos, dtl);
+                        max_t = dist;
+                    } else {                                       // DirLight::shine (light.cu:72-77)
+                        dtl = neg(L.v);
+                        to = make_ray(hpos, dtl);
+                        max_t = INFINITY;
+                    }
+                    rv = L.col;                                    // Light::attenuate (light.cu:30-31)
+                    q = make_ray(at(to, THRESH), to.d);
+                    dbg(P, me, 4);
+                    st = ST_WAIT_SHADOW;
+                } else {
+                    acc = acc + cur.atten * summed;                 // scene.cu:127
+                    if (pending_pop) { pending_pop = false; top--; if (top >= 0) cur = stk[top]; }
+                    st = top < 0 ? ST_DONE : ST_ADVANCE;
+                }
+                continue;
             }
-            const DMat& m = S.mats[is.mat];
-            if (cur.type == F_REFLECT) {                      // scene.cu:129-148
+            // ST_ADVANCE
+            if (cur.type == F_NORMAL) {                            // scene.cu:100-103
+                is_time = INFINITY;
+                dbg(P, me, 1);
+                q = cur.ray;
+                st = ST_WAIT_NORMAL;
+                continue;
+            }
+            const DMat& m = S.mats[is_mat];
+            bool do_pop = false;
+            if (cur.type == F_REFLECT) {                           // scene.cu:129-148
                 cur.type = F_REFRACT;
                 if (m.reflective) {
                     dbg(P, me, 2);
@@ -270,10 +381,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                     top++;
                     cur = c;
                 }
-                continue;
-            }
-            // F_REFRACT (scene.cu:149-184): reads the possibly clobbered shared Isect
-            if (m.refractive) {
+            } else if (m.refractive) {                            // F_REFRACT (scene.cu:149-184)
                 dbg(P, me, 3);
                 cur.type = F_NORMAL;
                 float n1, n2;
@@ -281,96 +389,80 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 else { n1 = 1.0f; n2 = S.mats[cur.last_mat].eta; }
                 bool tir;
                 V3 rd = refract(cur.ray.d, normalized(cur.norm), n1, n2, tir);
-                if (tir) pop();
+                if (tir) do_pop = true;
                 else { cur.ray = make_ray(cur.hit_pt, rd); cur.in_obj = !cur.in_obj; cur.depth--; }
             } else {
-                pop();
+                do_pop = true;
             }
+            if (do_pop) { top--; if (top >= 0) cur = stk[top]; else st = ST_DONE; }
         }
-    };
-    // Issue the shadow query of light `li`, or finish illuminate() when all lights are done.
-    auto next_light = [&]() {
-        if (li < S.n_lights) {
-            const DLight L = S.lights[li];
-            Ray to;
-            if (L.type == 0) {                                 // PointLight::shine (light.cu:63-70)
-                V3 disp = L.v - hpos;
-                float dist = len(disp);
-                float quad = P.dist_atten.x + P.dist_atten.y * dist + P.dist_atten.z * dist * dist;
-                da = quad < 1.0f ? 1.0f : 1.0f / quad;
-                dtl = normalized(disp);
-                to = make_ray(hpos, dtl);
-                max_t = dist;
-            } else {                                           // DirLight::shine (light.cu:72-77)
-                dtl = neg(L.v);
-                to = make_ray(hpos, dtl);
-                max_t = INFINITY;
-            }
-            rv = L.col;                                        // Light::attenuate (light.cu:29-61)
-            q = make_ray(at(to, THRESH), to.d);
-            dbg(P, me, 4);
-            phase = PH_SHADOW;
-            return;
-        }
-        acc = acc + cur.atten * summed;                         // scene.cu:127
-        if (pending_pop) { pending_pop = false; pop(); }
-        advance();
-    };
-    auto light_done = [&](V4 att) {
-        const DLight L = S.lights[li];
-        V4 inc = (L.type == 0) ? da * att : att;
-        summed = summed + phong(S.mats[is.mat], is.norm, inc, cur.ray.d, dtl);
-        li++;
-        next_light();
-    };
-
-    if (valid) {
-        cur.ray = r0; cur.hit_pt = v3(0, 0, 0); cur.norm = v3(0, 0, 0);
-        cur.atten = v4(1.0f, 1.0f, 1.0f, 1.0f); cur.last_mat = -1;
-        cur.type = F_NORMAL; cur.depth = P.depth; cur.in_obj = 0;
-        top = 0;
-        advance();
-    }
-    for (;;) {
-        const bool need = (phase == PH_NORMAL || phase == PH_SHADOW);
+        // ---- the wave-collective closest-hit query ----
+        const bool need = (st == ST_WAIT_NORMAL || st == ST_WAIT_SHADOW);
         if (!__ballot(need)) break;
-        Hit h;
-        h.time = INFINITY; h.norm = is.norm; h.mat = is.mat; h.inst = -1; h.tri = -1;
-        bool hit = cast_ray(S, need, q, h, cnt);
+        Best b;
+        b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
+        const bool hit = closest_hit(S, bv, need, q, b, wc);
         if (!need) continue;
-        if (phase == PH_NORMAL) {
-            if (primary) { primary = false; if (hit) { hinst = h.inst; htri = h.tri; } }
-            if (!hit) { is.time = INFINITY; pop(); advance(); continue; }
-            is.time = h.time; is.norm = h.norm; is.mat = h.mat;
-            if (cur.depth > 0) {                               // scene.cu:109-121
+        int hmat = 0;
+        V3 hn = v3(0, 0, 0);
+        if (hit) hn = hit_normal(S, bv, b, hmat);
+        if (st == ST_WAIT_NORMAL) {
+            if (primary) {
+                primary = false;
+                if (out_p >= 0) {
+                    if (P.hit_inst) P.hit_inst[out_p] = hit ? b.inst : -1;
+                    if (P.hit_tri) P.hit_tri[out_p] = hit ? b.tri : -1;
+                }
+            }
+            if (!hit) {                                            // scene.cu:124-126
+                is_time = INFINITY;
+                top--;
+                if (top >= 0) { cur = stk[top]; st = ST_ADVANCE; } else st = ST_DONE;
+                continue;
+            }
+            is_time = b.time; is_norm = hn; is_mat = hmat;
+            if (cur.depth > 0) {                                   // scene.cu:109-121
                 if (cur.in_obj) {
-                    const V4 kt = S.mats[is.mat].Kt;           // trans_atten (scene.cu:14-22): time^Kt
-                    cur.atten = cur.atten * v4(pow_ref(is.time, kt.x), pow_ref(is.time, kt.y),
-                                               pow_ref(is.time, kt.z), pow_ref(is.time, kt.w));
+                    const V4 kt = S.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
+                    cur.atten = cur.atten * v4(pow_ref(is_time, kt.x), pow_ref(is_time, kt.y),
+                                               pow_ref(is_time, kt.z), pow_ref(is_time, kt.w));
                 }
                 cur.type = F_REFLECT;
-                cur.hit_pt = at(cur.ray, is.time);
-                cur.last_mat = is.mat;
-                cur.norm = is.norm;
+                cur.hit_pt = at(cur.ray, is_time);
+                cur.last_mat = is_mat;
+                cur.norm = is_norm;
             } else {
-                pending_pop = true;                            // popped after illumination (frame data still needed)
+                pending_pop = true;                                // popped after illumination (frame still needed)
             }
-            const DMat& m = S.mats[is.mat];                    // illuminate (phong.cu:42-53)
+            const DMat& m = S.mats[is_mat];                        // org_light (phong.cu:36-39)
             summed = m.Ke + m.Ka * P.ambience;
-            hpos = at(cur.ray, is.time);
             li = 0;
-            next_light();
-        } else {                                               // shadow segment result
-            if (!hit || h.time > max_t) { light_done(rv); continue; }
-            const DMat& m = S.mats[h.mat];
-            if (!m.refractive) { light_done(v4(0, 0, 0, 0)); continue; }
-            if (dot(h.norm, q.d) > 0) {                        // calc_shadow_atten (light.cu:18-25)
-                rv = rv * v4(pow_ref(m.Kt.x, h.time), pow_ref(m.Kt.y, h.time), pow_ref(m.Kt.z, h.time),
-                             pow_ref(m.Kt.w, h.time));
+            st = ST_LIGHT;
+            continue;
+        }
+        // ST_WAIT_SHADOW: one shadow segment (light.cu:35-58)
+        bool light_done = true;
+        V4 att = rv;
+        if (hit && !(b.time > max_t)) {
+            const DMat& m = S.mats[hmat];
+            if (!m.refractive) {
+                att = v4(0, 0, 0, 0);
+            } else {
+                if (dot(hn, q.d) > 0) {                            // calc_shadow_atten (light.cu:18-25)
+                    rv = rv * v4(pow_ref(m.Kt.x, b.time), pow_ref(m.Kt.y, b.time), pow_ref(m.Kt.z, b.time),
+                                 pow_ref(m.Kt.w, b.time));
+                }
+                q = make_ray(at(q, b.time), q.d);
+                max_t -= b.time;
+                dbg(P, me, 4);
+                light_done = false;
             }
-            q = make_ray(at(q, h.time), q.d);
-            max_t -= h.time;
-            dbg(P, me, 4);
+        }
+        if (light_done) {
+            const V4 inc = (S.lights[li].type == 0) ? da * att : att;   // PointLight: dist_atten * attenuate()
+            summed = summed + phong(S.mats[is_mat], is_norm, inc, cur.ray.d, dtl);
+            li++;
+            st = ST_LIGHT;
         }
     }
     return acc;
@@ -380,63 +472,79 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
     return v4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
 }
 
-// One wave = one group of `px_per_wave` pixels x `lanes_per_px` samples.  Lane
-// (pixel p, sub s) traces samples k = round*L + s; the group leader sums the
-// clamped sample radiance in k order (build-defined spp extension).
-template <int NS>
-__global__ __launch_bounds__(TRACE_BLOCK) void trace_kernel(TraceParams P, SceneView S) {
+// Persistent blocks (one per CU): the BVH and the instance records are staged in
+// LDS once, then every wave repeatedly takes a pixel group from the work counter.
+// A group = `px_per_wave` pixels x `lanes_per_px` samples; lane (pixel p, sub s)
+// traces samples k = round*L + s and the group leader sums the clamped sample
+// radiance in k order (build-defined spp extension).
+template <int NS, bool LDS>
+__global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    BvhRefs bv;
+    if (LDS) {
+        const int n2 = 2 * S.n_leaf;
+        float4* a = reinterpret_cast<float4*>(smem);
+        float2* b = reinterpret_cast<float2*>(smem + 16 * (size_t)n2);
+        int* lf = reinterpret_cast<int*>(smem + 24 * (size_t)n2);
+        float4* in = reinterpret_cast<float4*>(smem + (((24 * (size_t)n2 + 4 * (size_t)S.n_leaf) + 15) & ~(size_t)15));
+        for (int i = threadIdx.x; i < n2; i += blockDim.x) { a[i] = S.node_a[i]; b[i] = S.node_b[i]; }
+        for (int i = threadIdx.x; i < S.n_leaf; i += blockDim.x) lf[i] = S.leaf_inst[i];
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        __syncthreads();
+        bv.a = a; bv.b = b; bv.leaf = lf; bv.inst = in;
+    } else {
+        bv.a = S.node_a; bv.b = S.node_b; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    }
     const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
-    const int gx = g % P.n_gx, gy = g / P.n_gx;
-    const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
-    const bool valid = g < P.n_groups && pix < P.px_per_wave && px < P.W && pr < P.n_rows;
-    const int py = P.row0 + pr * P.row_step;
-    const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
-    Counters cnt{0, 0, 0, 0};
-    V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
-    int hinst = -1, htri = -1;
     const int rounds = (P.spp + L - 1) / L;
-    for (int rd = 0; rd < rounds; rd++) {
-        const int k = rd * L + sub;
-        const bool act = valid && k < P.spp;
-        Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
-        if (act) {
-            float2 o = P.spp_off[k];
-            r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
-        }
-        int hi, ht;
-        V4 c = trace_sample<NS>(P, S, act, r0, me && rd == 0, hi, ht, cnt);
-        if (rd == 0 && sub == 0) { hinst = hi; htri = ht; }
-        for (int s = 0; s < L; s++) {                          // in-order reduction over samples
-            V4 v = shfl4(c, base + s);
-            if (sub == 0 && rd * L + s < P.spp) {
-                sum_c = sum_c + v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y,
-                                   v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);   // raytracer.cu:37-40
-                sum_r = sum_r + v;
+    WaveCounters wc{0, 0, 0, 0};
+    for (;;) {
+        int g = 0;
+        if (lane == 0) g = atomicAdd(P.work, 1);
+        g = __shfl(g, 0);
+        if (g >= P.n_groups) break;
+        const int gx = g % P.n_gx, gy = g / P.n_gx;
+        const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
+        const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
+        const int py = P.row0 + pr * P.row_step;
+        const long p = P.compact ? (long)pr * P.W + px : (long)py * P.W + px;
+        const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
+        V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
+        for (int rd = 0; rd < rounds; rd++) {
+            const int k = rd * L + sub;
+            const bool act = valid && k < P.spp;
+            Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
+            if (act) {
+                float2 o = P.spp_off[k];
+                r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
+            }
+            V4 c = trace_sample<NS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? p : -1, wc);
+            for (int s = 0; s < L; s++) {                      // in-order reduction over samples
+                V4 v = shfl4(c, base + s);
+                if (sub == 0 && rd * L + s < P.spp) {
+                    sum_c = sum_c + v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y,
+                                       v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);   // raytracer.cu:37-40
+                    sum_r = sum_r + v;
+                }
             }
         }
-    }
-    if (valid && sub == 0) {
-        const float inv = (float)P.spp;
-        const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
-        // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
-        const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
-                             ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
-        const size_t p = P.compact ? (size_t)pr * P.W + px : (size_t)py * P.W + px;
-        if (P.rgba) P.rgba[p] = enc;
-        if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
-        if (P.hit_inst) P.hit_inst[p] = hinst;
-        if (P.hit_tri) P.hit_tri[p] = htri;
-    }
-    if (P.stats) {                                             // wave-reduced counters
-        unsigned long long v[4] = {cnt.rays, cnt.nodes, cnt.leaves, cnt.tris};
-        for (int i = 0; i < 4; i++) {
-            unsigned long long x = v[i];
-            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-            if (lane == 0 && x) atomicAdd(&P.stats[i], x);
+        if (valid && sub == 0) {
+            const float inv = (float)P.spp;
+            const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
+            // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
+            const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
+                                 ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
+            if (P.rgba) P.rgba[p] = enc;
+            if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
+    }
+    if (P.stats && lane == 0) {
+        if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
+        if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
+        if (wc.leaves) atomicAdd(&P.stats[2], wc.leaves);
+        if (wc.tris) atomicAdd(&P.stats[3], wc.tris);
     }
 }
 
@@ -451,7 +559,9 @@ struct BvhArgs {
     int n;                   // padded leaf count (power of two)
     Box* boxes;              // scratch: n instance boxes
     Box* tree;               // scratch: 2n-1 boxes, reference storage order
-    DNode* nodes;            // out: 2n entries (index 0 unused)
+    float4* node_a;          // out: [2n] heap order (index 0 unused): (mnx, mny, mnz, mxx)
+    float2* node_b;          // out: [2n] (mxy, mxz); degenerate boxes: min=+inf, max=-inf
+    int* leaf_inst;          // out: [n] instance of leaf node n+i
 };
 
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
@@ -510,11 +620,14 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     for (int k = tid + 1; k < 2 * n; k += nt) {
         const int s = 2 * n - 1 - k;
         const Box b = A.tree[s];
-        DNode d;
-        d.mnx = b.mn.x; d.mny = b.mn.y; d.mnz = b.mn.z; d.mxx = b.mx.x; d.mxy = b.mx.y; d.mxz = b.mx.z;
-        d.nd = b.nd;
-        d.inst = (k >= n) ? idx[s] : -1;
-        A.nodes[k] = d;
+        if (b.nd) {
+            A.node_a[k] = make_float4(b.mn.x, b.mn.y, b.mn.z, b.mx.x);
+            A.node_b[k] = make_float2(b.mx.y, b.mx.z);
+        } else {
+            A.node_a[k] = make_float4(INFINITY, INFINITY, INFINITY, -INFINITY);
+            A.node_b[k] = make_float2(-INFINITY, -INFINITY);
+        }
+        if (k >= n) A.leaf_inst[k - n] = idx[s];
     }
 }
 
@@ -584,7 +697,9 @@ struct rt_scene {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // device buffers
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
-    DLight* d_lights = nullptr; DNode* d_nodes = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
+    DLight* d_lights = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
+    float4* d_node_a = nullptr; float2* d_node_b = nullptr; int* d_leaf = nullptr; float4* d_inst4 = nullptr;
+    int* d_work = nullptr; int n_cu = 0;
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
     uint32_t* d_canvas = nullptr;
@@ -615,6 +730,8 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
     return n;
 }
 
+int upload_inst4(rt_scene* s);
+
 int upload(rt_scene* s) {
     if (s->uploaded) return RT_OK;
     int ndev = 0;
@@ -641,14 +758,34 @@ int upload(rt_scene* s) {
         return r;
     s->n_leaf = padded((int)h.d_insts.size());
     if (s->n_leaf > BVH_MAX_LEAVES) return fail(RT_ERR_LIMIT, "more than 8192 padded instances: single-workgroup BVH build limit");
+    s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
-    HIPCHK(hipMalloc((void**)&s->d_nodes, 2 * nl * sizeof(DNode)));
+    HIPCHK(hipMalloc((void**)&s->d_node_a, 2 * nl * sizeof(float4)));
+    HIPCHK(hipMalloc((void**)&s->d_node_b, 2 * nl * sizeof(float2)));
+    HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
+    HIPCHK(hipMalloc((void**)&s->d_work, 16 * sizeof(int)));
+    if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_stats, 4 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
+    return RT_OK;
+}
+
+// compact instance records for the trace kernel: (p, mesh | 0x80000000 when the pose is not identity)
+int upload_inst4(rt_scene* s) {
+    const rt::Scene& h = s->h;
+    std::vector<float4> v(h.d_insts.size());
+    for (size_t i = 0; i < v.size(); i++) {
+        const DInst& d = h.d_insts[i];
+        uint32_t w = (uint32_t)d.mesh | (d.pose.identity ? 0u : 0x80000000u);
+        float fw; memcpy(&fw, &w, 4);
+        v[i] = make_float4(d.pose.p.x, d.pose.p.y, d.pose.p.z, fw);
+    }
+    if (!v.empty()) HIPCHK(hipMemcpy(s->d_inst4, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice));
     return RT_OK;
 }
 
@@ -670,7 +807,8 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.insts = s->d_insts; A.n_inst = (int)s->h.d_insts.size();
     A.meshes = s->d_meshes; A.n_meshes = (int)s->h.d_meshes.size();
     A.tris = s->d_tris; A.n = s->n_leaf;
-    A.boxes = s->d_boxes; A.tree = s->d_tree; A.nodes = s->d_nodes;
+    A.boxes = s->d_boxes; A.tree = s->d_tree;
+    A.node_a = s->d_node_a; A.node_b = s->d_node_b; A.leaf_inst = s->d_leaf;
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
@@ -683,7 +821,8 @@ int build_bvh(rt_scene* s, hipStream_t st) {
 SceneView view_of(const rt_scene* s, bool use_bvh) {
     SceneView v;
     v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
-    v.nodes = s->d_nodes; v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
+    v.node_a = s->d_node_a; v.node_b = s->d_node_b; v.leaf_inst = s->d_leaf; v.inst4 = s->d_inst4;
+    v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
     return v;
 }
@@ -709,11 +848,27 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.gw = gw; P.gh = P.px_per_wave / gw;
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
-    dim3 grid((P.n_groups + (TRACE_BLOCK / 64) - 1) / (TRACE_BLOCK / 64));
+    P.work = s->d_work;
+    HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), st));
+    // LDS image: node_a[2n] | node_b[2n] | leaf_inst[n] | (16-B aligned) inst4[n_inst]
+    size_t lds = (24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15;
+    lds += 16 * (size_t)S.n_inst;
+    const bool use_lds = lds <= (size_t)LDS_LIMIT;
     const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
-    if (ns <= 0) hipLaunchKernelGGL(trace_kernel<0>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
-    else if (ns <= 2) hipLaunchKernelGGL(trace_kernel<2>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
-    else hipLaunchKernelGGL(trace_kernel<MAX_FRAMES - 1>, grid, dim3(TRACE_BLOCK), 0, st, P, S);
+    const void* fn;
+    if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true> : ns <= 2 ? (const void*)trace_kernel<2, true>
+                                                                       : (const void*)trace_kernel<MAX_FRAMES - 1, true>;
+    else fn = ns <= 0 ? (const void*)trace_kernel<0, false> : ns <= 2 ? (const void*)trace_kernel<2, false>
+                                                             : (const void*)trace_kernel<MAX_FRAMES - 1, false>;
+    const size_t shm = use_lds ? lds : 0;
+    if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
+    const int waves_needed = P.n_groups;
+    int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
+    blocks = std::max(blocks, 1);
+    void* args[] = {&P, &S};
+    HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st));
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
@@ -736,7 +891,8 @@ void invalidate(rt_scene* s) { s->bvh_valid = false; }
 
 rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
-    dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights); dfree(d_nodes);
+    dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
+    dfree(d_node_a); dfree(d_node_b); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -830,7 +986,11 @@ int rt_builder_set_trans(rt_scene* s, int t, const float* pos, const float* q) {
     if (q) s->h.insts[t].rot = Q{q[0], q[1], q[2], q[3]};
     if (s->finished) {   // instances moved after finishing: refresh the flat copy and the device copy
         s->h.d_insts[t].pose = make_pose(s->h.insts[t].rot, s->h.insts[t].pos);
-        if (s->uploaded) HIPCHK(hipMemcpy(s->d_insts + t, &s->h.d_insts[t], sizeof(DInst), hipMemcpyHostToDevice));
+        if (s->uploaded) {
+            HIPCHK(hipMemcpy(s->d_insts + t, &s->h.d_insts[t], sizeof(DInst), hipMemcpyHostToDevice));
+            int r = upload_inst4(s);
+            if (r != RT_OK) return r;
+        }
         invalidate(s);
     }
     return RT_OK;
