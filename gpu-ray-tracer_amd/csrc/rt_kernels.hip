@@ -117,9 +117,17 @@ struct BvhRefs {
     const float4* inst;     // [n_inst] (px, py, pz, mesh | 0x80000000 if the pose is not identity)
 };
 
-__device__ __forceinline__ bool node_hit(float4 A, float2 B, const Ray& r) {
+#ifndef RT_FILTERED
+#define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
+#endif
+
+__device__ __forceinline__ bool node_hit(float4 A, float2 B, const Ray& r, const RayInv& ri) {
     if (!(A.x <= A.w)) return false;                          // !nondegenerate (bounding_box.cu:63-65)
+#if RT_FILTERED
+    return box_hit_f(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r, ri);
+#else
     return box_hit(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r);
+#endif
 }
 
 struct Best { float time; int inst, tri; float u, v; };     // closest accepted triangle so far
@@ -157,7 +165,12 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
     for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
         const DTri T = ldc(S.tris, t);
         float time, u, v;
-        if (tri_accept(T, mr, t_best, time, u, v)) { t_best = time; best = t; bu = u; bv_ = v; }
+#if RT_FILTERED
+        const bool acc = tri_accept_f(T.a, T.b, T.c, T.pn, T.area, T.inv_area, mr, t_best, time, u, v);
+#else
+        const bool acc = tri_accept(T, mr, t_best, time, u, v);
+#endif
+        if (acc) { t_best = time; best = t; bu = u; bv_ = v; }
     }
     if (best < 0) return false;
     b.time = (t_best * scale) * dir_len;                      // fix_isect, then cast_local
@@ -199,8 +212,9 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         return hit;
     }
     const int n = S.n_leaf;
+    const RayInv ri = ray_inv(r);
     wc.nodes += __popcll(am);                                  // root test
-    const bool hr = active && node_hit(bv.a[1], bv.b[1], r);
+    const bool hr = active && node_hit(bv.a[1], bv.b[1], r, ri);
     const unsigned long long br = __ballot(hr);
     if (!br) return false;
     auto leaf = [&](bool h, int li) {
@@ -218,8 +232,8 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     unsigned pending = 0;
     for (;;) {
         const int c0 = 2 * k;
-        const bool h0 = active && node_hit(bv.a[c0], bv.b[c0], r);
-        const bool h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r);
+        const bool h0 = active && node_hit(bv.a[c0], bv.b[c0], r, ri);
+        const bool h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r, ri);
         if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
 #pragma nounroll
             for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : h1, c0 + c - n);
@@ -548,6 +562,51 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     }
 }
 
+
+// Experiment kernel (profiling aid, not on the product path): closest hit of the
+// primary rays only, persistent blocks with the BVH in LDS, one sample per lane.
+template <bool LDS>
+__global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams P, SceneView S, float4* out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    BvhRefs bv;
+    if (LDS) {
+        const int n2 = 2 * S.n_leaf;
+        float4* a = reinterpret_cast<float4*>(smem);
+        float2* b = reinterpret_cast<float2*>(smem + 16 * (size_t)n2);
+        int* lf = reinterpret_cast<int*>(smem + 24 * (size_t)n2);
+        float4* in = reinterpret_cast<float4*>(smem + (((24 * (size_t)n2 + 4 * (size_t)S.n_leaf) + 15) & ~(size_t)15));
+        for (int i = threadIdx.x; i < n2; i += blockDim.x) { a[i] = S.node_a[i]; b[i] = S.node_b[i]; }
+        for (int i = threadIdx.x; i < S.n_leaf; i += blockDim.x) lf[i] = S.leaf_inst[i];
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        __syncthreads();
+        bv.a = a; bv.b = b; bv.leaf = lf; bv.inst = in;
+    } else {
+        bv.a = S.node_a; bv.b = S.node_b; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    }
+    const int lane = threadIdx.x & 63;
+    const int L = P.lanes_per_px;
+    const int pix = lane / L, sub = lane - pix * L;
+    WaveCounters wc{0, 0, 0, 0};
+    for (;;) {
+        int g = 0;
+        if (lane == 0) g = atomicAdd(P.work, 1);
+        g = __shfl(g, 0);
+        if (g >= P.n_groups) break;
+        const int gx = g % P.n_gx, gy = g / P.n_gx;
+        const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
+        const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows && sub < P.spp;
+        const int py = P.row0 + pr * P.row_step;
+        Ray r{v3(0, 0, 0), v3(0, 0, 1)};
+        if (valid) { float2 o = P.spp_off[sub]; r = camera_at(P.cam, (float)px + o.x, (float)py + o.y); }
+        Best b; b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0; b.v = 0;
+        bool h = closest_hit(S, bv, valid, r, b, wc);
+        if (valid) out[((size_t)pr * P.W + px) * P.lanes_per_px + sub] = make_float4(h ? b.time : -1.0f, __int_as_float(b.inst), b.u, b.v);
+    }
+    if (P.stats && lane == 0) {
+        atomicAdd(&P.stats[0], wc.rays); atomicAdd(&P.stats[1], wc.nodes);
+        atomicAdd(&P.stats[2], wc.leaves); atomicAdd(&P.stats[3], wc.tris);
+    }
+}
 // ---------------------------------------------------------------------------
 // BVH build: ropt::gpu::BVH::BVH (bvh.cu:74-91) + create_boxes (raytracer.cu:54-74)
 // in one workgroup.  Output: heap-ordered nodes[1 .. 2n-1].
@@ -680,6 +739,23 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
             break;
         }
         case 12: of[i] = pow_ref(a[i], b[i]); break;
+        case 13: {   // filtered triangle test (best = +inf): must equal the exact test bit for bit
+            const float* t = a + 9 * i;
+            V3 A = L3(t), B = L3(t + 3), C = L3(t + 6);
+            V3 pn = cross(B - A, C - A);
+            float area = len(pn);
+            Ray r = make_ray(L3(b + 6 * i), L3(b + 6 * i + 3));
+            float tm = NAN, u = NAN, v = NAN;
+            bool h = tri_accept_f(A, B, C, normalized(pn), area, 1.0f / area, r, INFINITY, tm, u, v);
+            oi[i] = h; of[3 * i] = h ? tm : NAN; of[3 * i + 1] = h ? u : NAN; of[3 * i + 2] = h ? v : NAN;
+            break;
+        }
+        case 14: {   // filtered box test
+            const float* bx = a + 7 * i;
+            Ray r = make_ray(L3(b + 6 * i), L3(b + 6 * i + 3));
+            oi[i] = bx[6] != 0 && box_hit_f(L3(bx), L3(bx + 3), r, ray_inv(r));
+            break;
+        }
         default: break;
     }
 }
@@ -1265,15 +1341,63 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
     return RT_OK;
 }
 
+// Profiling aid (not part of rt_amd.h's stable surface): run experiment `which`
+// (0 = primary-ray closest-hit only) `reps` times; returns mean kernel ms and counters.
+int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_t* counters) {
+    CHECK_FINISHED(s);
+    int r;
+    if ((r = upload(s)) != RT_OK) return r;
+    HIPCHK(hipSetDevice(s->device));
+    if ((r = ensure_spp(s, spp)) != RT_OK) return r;
+    if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+    rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
+    TraceParams P{};
+    const rt::Scene& h = s->h;
+    P.cam = h.d_cam; P.W = h.cam.W; P.H = h.cam.H; P.row0 = 0; P.row_step = 1; P.n_rows = P.H; P.spp = spp;
+    P.spp_off = s->d_spp; P.stats = s->d_stats; P.work = s->d_work;
+    P.lanes_per_px = std::min(spp, 64); P.px_per_wave = 64 / P.lanes_per_px;
+    int gw = 1; while (gw * gw < P.px_per_wave) gw <<= 1;
+    P.gw = gw; P.gh = P.px_per_wave / gw; P.n_gx = (P.W + P.gw - 1) / P.gw;
+    P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
+    SceneView S = view_of(s, true);
+    size_t lds = ((24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + 16 * (size_t)S.n_inst;
+    const void* fn = (const void*)primary_only_kernel<true>;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    int blocks = s->n_cu * per_cu;
+    float4* out = nullptr;
+    HIPCHK(hipMalloc((void**)&out, (size_t)P.W * P.H * P.lanes_per_px * sizeof(float4)));
+    float total = 0;
+    for (int i = 0; i < reps; i++) {
+        HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), s->stream));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), s->stream));
+        HIPCHK(hipEventRecord(s->ev[0], s->stream));
+        void* args[] = {&P, &S, &out};
+        HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, s->stream));
+        HIPCHK(hipEventRecord(s->ev[1], s->stream));
+        HIPCHK(hipEventSynchronize(s->ev[1]));
+        float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
+        if (i > 0 || reps == 1) total += t;
+    }
+    unsigned long long v[4];
+    HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    if (counters) for (int i = 0; i < 4; i++) counters[i] = v[i];
+    if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
+    (void)hipFree(out);
+    (void)which;
+    return RT_OK;
+}
+
 int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2, float* of, int32_t* oi,
                   uint64_t* ou) {
     static const char* ops[] = {"normalize3", "cross", "reflect", "refract", "quat_rotate", "quat_inverse", "quat_mul",
-                                "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow"};
+                                "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow", "tri_hit_f", "box_hit_f"};
     // per-op sizes (floats): in0, in1, in2, out_f, out_i, out_u per element
     static const int sz[][6] = {{3, 0, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 2, 3, 1, 0},
                                 {4, 3, 0, 3, 0, 0}, {4, 0, 0, 4, 0, 0}, {4, 4, 0, 4, 0, 0}, {9, 6, 0, 3, 1, 0},
                                 {6, 0, 0, 6, 0, 0}, {3, 0, 0, 0, 0, 1}, {4, 0, 0, 9, 0, 0}, {7, 6, 0, 0, 1, 0},
-                                {1, 1, 0, 1, 0, 0}};
+                                {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}};
     if (!op || n <= 0) return fail(RT_ERR_ARG, "bad arguments");
     int k = -1;
     for (int i = 0; i < (int)(sizeof ops / sizeof *ops); i++) if (!strcmp(op, ops[i])) k = i;

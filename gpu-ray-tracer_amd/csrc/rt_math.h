@@ -216,6 +216,86 @@ RT_HD bool tri_hit(V3 a, V3 b, V3 c, V3 pn, float area, const Ray& r, float& tim
     return false;
 }
 
+// ---- exactness-preserving filtered tests (device) ----------------------------
+// The reference's box and triangle tests are decided by comparisons of correctly
+// rounded quotients and square roots.  The filtered forms evaluate cheap
+// approximations with a rigorous error bound and return the reference's exact
+// answer whenever the approximation is decisive; inside the (tiny) uncertainty
+// band they run the exact reference arithmetic.  Derivation (u = 2^-24):
+//  * q' = fl(e * fl(1/d)) vs q = fl(e / d): |q' - q| <= 3.0001 u |e/d| in the
+//    normal range; the bound used is 16 u max|q'| + 2^-120 (absolute floor for
+//    the subnormal range; non-finite values always fall back).  min/max of
+//    perturbed values move by at most the same bound, and the slab test's
+//    early exits are monotone, so its outcome is (T_min <= T_max && T_max >= 1e-5)
+//    evaluated once at the end.
+//  * v_sqrt_f32 / v_rcp_f32 are within 1 ulp; a barycentric term b' =
+//    fl(sqrt'(s) * fl(1/area)) is within 6u of fl(fl(sqrt(s)) / area); the sum
+//    test uses a 32u margin.  The accepted (t, u, v) are always recomputed exactly.
+struct RayInv { float ix, iy, iz; int exact; };
+RT_HD RayInv ray_inv(const Ray& r) {
+    RayInv v;
+    v.ix = r.d.x != 0 ? 1.0f / r.d.x : 0.0f;
+    v.iy = r.d.y != 0 ? 1.0f / r.d.y : 0.0f;
+    v.iz = r.d.z != 0 ? 1.0f / r.d.z : 0.0f;
+    v.exact = !(isfinite(v.ix) && isfinite(v.iy) && isfinite(v.iz));
+    return v;
+}
+constexpr float FILT_BOX = 0x1p-20f;       // 16 u
+constexpr float FILT_TRI = 0x1p-19f;       // 32 u
+constexpr float FILT_ABS = 0x1p-120f;
+
+RT_HD void slab_axis_f(float mn, float mx, float o, float d, float inv, float& tmin, float& tmax, float& m) {
+    if (d == 0) return;
+    float q0 = (mn - o) * inv, q1 = (mx - o) * inv;
+    tmin = fmaxf(tmin, fminf(q0, q1));
+    tmax = fminf(tmax, fmaxf(q0, q1));
+    m = fmaxf(m, fmaxf(fabsf(q0), fabsf(q1)));
+}
+RT_HD bool box_hit_f(V3 mn, V3 mx, const Ray& r, const RayInv& ri) {
+    if (ri.exact) return box_hit(mn, mx, r);
+    float tmin = -INFINITY, tmax = INFINITY, m = 0.0f;
+    slab_axis_f(mn.x, mx.x, r.o.x, r.d.x, ri.ix, tmin, tmax, m);
+    slab_axis_f(mn.y, mx.y, r.o.y, r.d.y, ri.iy, tmin, tmax, m);
+    slab_axis_f(mn.z, mx.z, r.o.z, r.d.z, ri.iz, tmin, tmax, m);
+    const float E = m * FILT_BOX + FILT_ABS;
+    if (tmin - tmax > 2.0f * E || tmax + E < THRESH) return false;     // certainly a miss
+    if (tmin + 2.0f * E <= tmax && tmax - E >= THRESH) return true;      // certainly a hit
+    return box_hit(mn, mx, r);                                           // near a tie: exact
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+#else
+inline float fast_sqrt(float x) { return sqrtf(x); }
+inline float fast_rcp(float x) { return 1.0f / x; }
+#endif
+
+// tri_hit (above) + TriInner::tri_hit's acceptance (trimesh.cu:56), filtered.
+// inv_area = fl(1 / area) (host-precomputed; only used by the filter).
+RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, const Ray& r, float best,
+                        float& time, float& u, float& v) {
+    float denom = dot(r.d, pn);
+    if (fabsf(denom) < THRESH) return false;
+    float num = dot(a - r.o, pn);
+    float ta = num * fast_rcp(denom);                    // ~1 ulp of the exact fl(fl(1/denom) * num)
+    float et = fabsf(ta) * FILT_TRI + FILT_ABS;
+    if (ta + et < THRESH || ta - et >= best) return false;  // certainly rejected by t >= 1e-5 && t < best
+    float t = (1.0f / denom) * num;                       // exact (geometry.h:259)
+    if (!(t >= THRESH && t < best)) return false;
+    V3 p = at(r, t);
+    V3 x0 = cross(c - p, b - p), x1 = cross(c - p, a - p), x2 = cross(a - p, b - p);
+    float s0 = dot(x0, x0), s1 = dot(x1, x1), s2 = dot(x2, x2);
+    float sum = (fast_sqrt(s0) * inv_area + fast_sqrt(s1) * inv_area) + fast_sqrt(s2) * inv_area;
+    float dev = fabsf(sum - 1.0f), eb = sum * FILT_TRI + FILT_ABS;
+    if (!(dev <= THRESH + eb)) return false;             // certainly outside (also catches NaN)
+    float b1 = sqrtf(s1) / area, b2 = sqrtf(s2) / area;  // exact barycentrics (geometry.h:281-283)
+    if (dev < THRESH - eb) { time = t; u = b1; v = b2; return true; }   // certainly inside
+    float b0 = sqrtf(s0) / area;
+    if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
+    return false;
+}
+
 // ---- quaternion <-> basis (geometry.h:36-41, 183-198) ----
 inline Q axis_angle_gxx(V3 axis, float theta) {   // g++ TU (cube_world.cc): double cos/sin
     float hc = (float)cos((double)(0.5f * theta));

@@ -248,6 +248,7 @@ int Scene::flatten(std::string* err) {
             V3 pn = cross(d.b - d.a, d.c - d.a);                 // Triangle::hit (geometry.h:275-276)
             d.pn = normalized(pn);                               // Plane ctor (geometry.h:233)
             d.area = len(pn);                                    // geometry.h:280
+            d.inv_area = 1.0f / d.area;
             d.mat = tr.mat;
             d.n0 = norms[tr.i0]; d.n1 = norms[tr.i1]; d.n2 = norms[tr.i2];
             d_tris.push_back(d);

@@ -34,12 +34,12 @@ struct CameraDesc {
 };
 
 // ---- device-ready records (all plain-old-data, 16-byte aligned) ----
-struct alignas(16) DTri {              // 96 B: hot part first (13 floats read per test)
+struct alignas(16) DTri {              // 96 B: hot part first (14 floats read per test)
     rtm::V3 a, b, c, pn;               // vertices (mesh-local), normalized plane normal
     float area;                        // |cross(b-a, c-a)|
-    int mat;
+    float inv_area;                    // fl(1/area): only used by the filtered test's estimate
     rtm::V3 n0, n1, n2;                // vertex normals (generate_normals)
-    int pad[2];
+    int mat, pad;
 };
 struct alignas(16) DMesh { rtm::Pose pose; int tri_begin, tri_count, pad[2]; };
 struct alignas(16) DInst { rtm::Pose pose; int mesh, pad[3]; };

@@ -87,3 +87,58 @@ def test_device_pow_within_one_ulp(gpu):
     ref = np.power(x.astype(np.float64), y.astype(np.float64)).astype(np.float32)
     ulp = np.abs(out.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
     assert ulp.max() <= 1
+
+
+def test_filtered_triangle_equals_exact(gpu):
+    """tri_accept_f (filtered) == Triangle::hit + the t >= 1e-5 acceptance, bit for bit, on the
+    edge-dense golden vectors (the reference's own geometry.h produced them)."""
+    k = g("tri_hit")
+    out, hit = gpu.kat_device("tri_hit_f", k["tri"], k["ray"])
+    exp_hit = (k["hit"] == 1) & (k["out"][:, 0] >= np.float32(1e-5))
+    assert np.array_equal(hit.astype(bool), exp_hit)
+    assert np.array_equal(_bits(out[exp_hit]), _bits(k["out"][exp_hit]))
+
+
+def _adversarial_boxes(rng, n):
+    mn = (rng.normal(size=(n, 3)) * 4).astype(np.float32)
+    mx = (mn + np.abs(rng.normal(size=(n, 3))) + np.float32(1e-3)).astype(np.float32)
+    box = np.concatenate([mn, mx, np.ones((n, 1), np.float32)], 1)
+    o = (rng.normal(size=(n, 3)) * 20).astype(np.float32)
+    # targets exactly on faces, edges and corners (the slab test's ties)
+    t = rng.uniform(-0.05, 1.05, size=(n, 3)).astype(np.float32)
+    snap = rng.random((n, 3))
+    t[snap < 0.3] = 0.0
+    t[(snap >= 0.3) & (snap < 0.6)] = 1.0
+    tgt = (mn + (mx - mn) * t).astype(np.float32)
+    d = (tgt - o).astype(np.float32)
+    d[rng.random((n, 3)) < 0.03] = 0.0
+    return box, np.concatenate([o, d], 1).astype(np.float32)
+
+
+def test_filtered_box_equals_exact(gpu, oracle):
+    rng = np.random.default_rng(2024)
+    box, ray = _adversarial_boxes(rng, 200000)
+    ref, _ = oracle.kat("box_hit", box, ray)
+    assert np.array_equal(gpu.kat_device("box_hit_f", box, ray), ref)
+    assert np.array_equal(gpu.kat_device("box_hit", box, ray), ref)
+    assert 0.2 < ref.mean() < 0.9
+
+
+def test_filtered_triangle_adversarial(gpu, oracle):
+    """Rays aimed at triangle vertices/edges (barycentric sum right at the 1e-5 boundary)."""
+    rng = np.random.default_rng(99)
+    n = 100000
+    tri = (rng.normal(size=(n, 3, 3)) * 2).astype(np.float32)
+    w = rng.dirichlet([1, 1, 1], size=n).astype(np.float32)
+    e = rng.integers(0, 3, n)
+    w[np.arange(n), e] = rng.normal(scale=3e-6, size=n)      # just inside / outside an edge
+    p = np.einsum("ni,nij->nj", w, tri).astype(np.float32)
+    o = (p + rng.normal(size=(n, 3)) * 5).astype(np.float32)
+    ray = np.concatenate([o, p - o], 1).astype(np.float32)
+    tri = tri.reshape(n, 9)
+    h_ref, tuv = oracle.kat("tri_hit", tri, ray)
+    exp = (h_ref == 1) & (tuv[:, 0] >= np.float32(1e-5))
+    out, hit = gpu.kat_device("tri_hit_f", tri, ray)
+    assert np.array_equal(hit.astype(bool), exp)
+    assert np.array_equal(_bits(out[exp]), _bits(tuv[exp]))
+    assert 0.1 < exp.mean() < 0.9
