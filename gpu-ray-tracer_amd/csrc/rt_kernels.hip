@@ -198,8 +198,16 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 // Each lane processes exactly the leaves its own ray hits, in the reference's
 // DFS order, so results equal the single-ray semantics; counters are the
 // single-ray node tests (1 + 2 per internal node hit).
-__device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active, const Ray& r,
-                                            Best& b, WaveCounters& wc) {
+// `occl_t` >= 0 enables the occlusion early exit (shadow rays, all-opaque scenes): a
+// lane stops once it has accepted a hit with time <= occl_t = max_t * (1 - 8u).
+// The reference's closest hit is then also <= max_t and opaque (every later accept
+// is < that time up to the instance/mesh rescaling, |scale - 1| <= 4u), so
+// Light::attenuate returns 0 either way (light.cu:39-45).  Counters then count
+// the work done, so it is only used when statistics are not requested.
+template <bool NOLEAF = false>
+__device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
+                                            Best& b, WaveCounters& wc, float occl_t = -1.0f) {
+    bool active = active_in;
     const unsigned long long am = __ballot(active);
     wc.rays += __popcll(am);
     bool hit = false;
@@ -223,7 +231,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         const int ti = uni(bv.leaf[li]);                       // leaf instance: wave-uniform
         wc.leaves += __popcll(m);
         wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
-        if (h && cast_local(S, bv, ti, r, b)) hit = true;
+        if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
+        else if (h && cast_local(S, bv, ti, r, b)) {
+            hit = true;
+            if (b.time <= occl_t) active = false;             // occluded: this lane is done
+        }
     };
     if (n == 1) { leaf(hr, 0); return hit; }
     // one copy of the leaf code for both children (keeps the kernel small)
@@ -237,6 +249,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
 #pragma nounroll
             for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : h1, c0 + c - n);
+            if (!__ballot(active)) break;                      // every lane occluded
         } else {
             const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
             wc.nodes += 2ull * (__popcll(b0) + __popcll(b1));
@@ -287,6 +300,7 @@ struct TraceParams {
     int* hit_tri;
     unsigned long long* stats;
     int* work;                // persistent-wave work counter (zeroed before each launch)
+    int occl_exit;            // shadow-ray occlusion early exit (all-opaque scene, no statistics)
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
 };
@@ -415,7 +429,9 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         if (!__ballot(need)) break;
         Best b;
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
-        const bool hit = closest_hit(S, bv, need, q, b, wc);
+        float occl = -1.0f;
+        if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
+        const bool hit = closest_hit(S, bv, need, q, b, wc, occl);
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
@@ -514,11 +530,11 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     const int rounds = (P.spp + L - 1) / L;
     WaveCounters wc{0, 0, 0, 0};
-    for (;;) {
-        int g = 0;
-        if (lane == 0) g = atomicAdd(P.work, 1);
-        g = __shfl(g, 0);
-        if (g >= P.n_groups) break;
+    // Static, strided group assignment: wave w takes groups w, w + n_waves, ...  (a single
+    // global work counter serialised ~260k atomics per frame and cost ~2.5 ms; measured)
+    const int wave_id = blockIdx.x * (TRACE_BLOCK_P / 64) + (threadIdx.x >> 6);
+    const int n_waves = gridDim.x * (TRACE_BLOCK_P / 64);
+    for (int g = wave_id; g < P.n_groups; g += n_waves) {
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
         const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
@@ -565,7 +581,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
 
 // Experiment kernel (profiling aid, not on the product path): closest hit of the
 // primary rays only, persistent blocks with the BVH in LDS, one sample per lane.
-template <bool LDS>
+template <bool LDS, bool NOLEAF, int WORK>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams P, SceneView S, float4* out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     BvhRefs bv;
@@ -587,10 +603,17 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L;
     WaveCounters wc{0, 0, 0, 0};
+    const int wave_id = blockIdx.x * (TRACE_BLOCK_P / 64) + (threadIdx.x >> 6);
+    const int n_waves = gridDim.x * (TRACE_BLOCK_P / 64);
+    int g = WORK == 0 ? 0 : wave_id - n_waves;
     for (;;) {
-        int g = 0;
-        if (lane == 0) g = atomicAdd(P.work, 1);
-        g = __shfl(g, 0);
+        if (WORK == 0) {                     // one atomic per group
+            int t = 0;
+            if (lane == 0) t = atomicAdd(P.work, 1);
+            g = __shfl(t, 0);
+        } else {                             // static stride
+            g += n_waves;
+        }
         if (g >= P.n_groups) break;
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
@@ -599,7 +622,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams
         Ray r{v3(0, 0, 0), v3(0, 0, 1)};
         if (valid) { float2 o = P.spp_off[sub]; r = camera_at(P.cam, (float)px + o.x, (float)py + o.y); }
         Best b; b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0; b.v = 0;
-        bool h = closest_hit(S, bv, valid, r, b, wc);
+        bool h = closest_hit<NOLEAF>(S, bv, valid, r, b, wc);
         if (valid) out[((size_t)pr * P.W + px) * P.lanes_per_px + sub] = make_float4(h ? b.time : -1.0f, __int_as_float(b.inst), b.u, b.v);
     }
     if (P.stats && lane == 0) {
@@ -903,7 +926,13 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     return v;
 }
 
-int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y) {
+bool opaque_scene(const rt_scene* s) {
+    for (const DMat& m : s->h.d_mats) if (m.refractive) return false;
+    return true;
+}
+
+int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y,
+                 bool want_stats) {
     TraceParams P{};
     const rt::Scene& h = s->h;
     P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
@@ -913,7 +942,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.compact = o.compact; P.spp = o.spp; P.depth = h.depth;
     P.spp_off = s->d_spp;
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
-    P.stats = s->d_stats; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
+    P.stats = want_stats ? s->d_stats : nullptr; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
     SceneView S = view_of(s, o.use_bvh != 0);
     // sample-parallel mapping: L lanes per pixel (one sample each per round), 64/L pixels per wave
     P.lanes_per_px = std::min(o.spp, 64);
@@ -925,7 +954,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     P.work = s->d_work;
-    HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), st));
+    P.occl_exit = (opaque_scene(s) && !want_stats) ? 1 : 0;
     // LDS image: node_a[2n] | node_b[2n] | leaf_inst[n] | (16-B aligned) inst4[n_inst]
     size_t lds = (24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15;
     lds += 16 * (size_t)S.n_inst;
@@ -1250,7 +1279,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         oo.hit_tri = o->hit_tri ? (int32_t*)s->d_out[3] : nullptr;
     }
     uint32_t* rgba = oo.rgba ? oo.rgba : s->d_canvas;
-    if ((r = launch_trace(s, oo, st, rgba, nullptr, -1, -1)) != RT_OK) return r;
+    if ((r = launch_trace(s, oo, st, rgba, nullptr, -1, -1, timed)) != RT_OK) return r;
     if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
     if (te) HIPCHK(hipEventRecord(te[2], st));
     if (o->sync || timed || o->host_outputs) HIPCHK(hipStreamSynchronize(st));
@@ -1328,7 +1357,7 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
     rt_render_opts o;
     rt_render_opts_default(&o);
     o.row0 = y; o.row_step = s->h.cam.H;                                  // just the row of (x, y)
-    if ((r = launch_trace(s, o, s->stream, s->d_canvas, s->d_dbg, x, y)) != RT_OK) return r;
+    if ((r = launch_trace(s, o, s->stream, s->d_canvas, s->d_dbg, x, y, true)) != RT_OK) return r;
     std::vector<int> log(4096);
     HIPCHK(hipStreamSynchronize(s->stream));
     HIPCHK(hipMemcpy(log.data(), s->d_dbg, log.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -1361,7 +1390,10 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     SceneView S = view_of(s, true);
     size_t lds = ((24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + 16 * (size_t)S.n_inst;
-    const void* fn = (const void*)primary_only_kernel<true>;
+    const void* fn = which == 1 ? (const void*)primary_only_kernel<true, true, 0>
+                   : which == 2 ? (const void*)primary_only_kernel<true, true, 1>
+                   : which == 3 ? (const void*)primary_only_kernel<true, false, 1>
+                                : (const void*)primary_only_kernel<true, false, 0>;
     if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, lds) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -1385,7 +1417,6 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     if (counters) for (int i = 0; i < 4; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
-    (void)which;
     return RT_OK;
 }
 

@@ -125,3 +125,17 @@ def test_empty_scene_renders_black(gpu, tmp_path):
     s = gpu.Scene.load_json(str(p))
     fr = s.render(want=("rgba", "hit_inst"))
     assert (fr["rgba"] == 0).all() and (fr["hit_inst"] == -1).all()
+
+
+@pytest.mark.parametrize("scene,spp", [("world8_stress", 4), ("world16", 1), ("world1", 2)])
+def test_occlusion_early_exit_is_exact(gpu, oracle, scene, spp):
+    """Frames rendered without statistics use the shadow-ray occlusion early exit (all-opaque
+    scenes); they must equal the counted (full closest-hit) frames and the oracle."""
+    s = gpu.Scene.load_json(scene_path(scene), 240, 160)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    fast = s.render(spp=spp, want=want, stats=False)
+    full = s.render(spp=spp, want=want, stats=True)
+    for k in want:
+        assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
+    o = oracle.render(oracle.load(scene_path(scene), 240, 160), spp=spp, nthreads=8)
+    check_frame(fast, o, spp)
