@@ -50,6 +50,7 @@ constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
 constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
 constexpr int TRACE_BLOCK_P = 1024;      // persistent block: 16 waves sharing one LDS copy of the BVH
 constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
+constexpr int NQ = 8;                    // work queues (one per XCD dispatch slot), 64-B apart
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -530,11 +531,26 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     const int rounds = (P.spp + L - 1) / L;
     WaveCounters wc{0, 0, 0, 0};
-    // Static, strided group assignment: wave w takes groups w, w + n_waves, ...  (a single
-    // global work counter serialised ~260k atomics per frame and cost ~2.5 ms; measured)
-    const int wave_id = blockIdx.x * (TRACE_BLOCK_P / 64) + (threadIdx.x >> 6);
-    const int n_waves = gridDim.x * (TRACE_BLOCK_P / 64);
-    for (int g = wave_id; g < P.n_groups; g += n_waves) {
+    // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
+    // a wave drains its own queue (c = block % NQ, i.e. one per XCD dispatch slot) then the
+    // others.  The next ticket is requested one group ahead so the atomic's latency hides
+    // behind the current group; a single global counter serialised ~260k atomics (~2.5 ms,
+    // measured) and a static split left a 1.5x load-imbalance tail (measured).
+    const int q0 = blockIdx.x % NQ;
+    const int per_q = (P.n_groups + NQ - 1) / NQ;
+    int qi = 0;
+    auto take = [&](int q) {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&P.work[16 * ((q0 + q) % NQ)], 1);
+        return __shfl(t, 0);
+    };
+    int ticket = take(0);
+    for (;;) {
+        while (qi < NQ && ticket >= per_q) { qi++; if (qi < NQ) ticket = take(qi); }
+        if (qi >= NQ) break;
+        const int g = ((q0 + qi) % NQ) + NQ * ticket;
+        ticket = take(qi);                                     // prefetch the next ticket
+        if (g >= P.n_groups) continue;
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
         const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
@@ -863,7 +879,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_node_b, 2 * nl * sizeof(float2)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&s->d_work, 16 * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&s->d_work, 16 * NQ * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
@@ -932,7 +948,7 @@ bool opaque_scene(const rt_scene* s) {
 }
 
 int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y,
-                 bool want_stats) {
+                 bool want_stats, int occl_force = -1) {
     TraceParams P{};
     const rt::Scene& h = s->h;
     P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
@@ -954,7 +970,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     P.work = s->d_work;
-    P.occl_exit = (opaque_scene(s) && !want_stats) ? 1 : 0;
+    P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
+    HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
     // LDS image: node_a[2n] | node_b[2n] | leaf_inst[n] | (16-B aligned) inst4[n_inst]
     size_t lds = (24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15;
     lds += 16 * (size_t)S.n_inst;
@@ -1371,10 +1388,34 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
 }
 
 // Profiling aid (not part of rt_amd.h's stable surface): run experiment `which`
-// (0 = primary-ray closest-hit only) `reps` times; returns mean kernel ms and counters.
+// (0/3 = primary-ray closest-hit only (atomic / static work), 1/2 = same without leaf
+// work, 4 = full trace with the occlusion early exit AND counters: the work actually
+// done) `reps` times; returns mean kernel ms and counters.
 int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_t* counters) {
     CHECK_FINISHED(s);
     int r;
+    if (which == 4) {
+        if ((r = upload(s)) != RT_OK) return r;
+        HIPCHK(hipSetDevice(s->device));
+        if ((r = ensure_spp(s, spp)) != RT_OK) return r;
+        rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
+        if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+        float total = 0;
+        for (int i = 0; i < reps; i++) {
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), s->stream));
+            HIPCHK(hipEventRecord(s->ev[0], s->stream));
+            if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, 1)) != RT_OK) return r;
+            HIPCHK(hipEventRecord(s->ev[1], s->stream));
+            HIPCHK(hipEventSynchronize(s->ev[1]));
+            float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
+            if (i > 0 || reps == 1) total += t;
+        }
+        unsigned long long v[4];
+        HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
+        if (counters) for (int i = 0; i < 4; i++) counters[i] = v[i];
+        if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
+        return RT_OK;
+    }
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, spp)) != RT_OK) return r;
