@@ -48,7 +48,10 @@ namespace {
 
 constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
 constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
-constexpr int TRACE_BLOCK_P = 1024;      // persistent block: 16 waves sharing one LDS copy of the BVH
+#ifndef RT_BLOCK
+#define RT_BLOCK 768
+#endif
+constexpr int TRACE_BLOCK_P = RT_BLOCK;  // persistent block: 12 waves (3 per SIMD, 168-VGPR budget) sharing one LDS BVH copy
 constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
 constexpr int NQ = 8;                    // work queues (one per XCD dispatch slot), 64-B apart
 
