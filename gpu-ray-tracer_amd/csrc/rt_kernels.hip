@@ -208,24 +208,26 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 // is < that time up to the instance/mesh rescaling, |scale - 1| <= 4u), so
 // Light::attenuate returns 0 either way (light.cu:39-45).  Counters then count
 // the work done, so it is only used when statistics are not requested.
-template <bool NOLEAF = false>
+template <bool NOLEAF, bool STATS>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f) {
     bool active = active_in;
     const unsigned long long am = __ballot(active);
-    wc.rays += __popcll(am);
+    if (STATS) wc.rays += __popcll(am);
     bool hit = false;
     if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
         for (int i = 0; i < S.n_inst; i++) {
-            wc.leaves += __popcll(am);
-            wc.tris += (unsigned long long)__popcll(am) * ldc(S.meshes, uni(__float_as_int(bv.inst[i].w) & 0x7fffffff)).tri_count;
+            if (STATS) {
+                wc.leaves += __popcll(am);
+                wc.tris += (unsigned long long)__popcll(am) * ldc(S.meshes, uni(__float_as_int(bv.inst[i].w) & 0x7fffffff)).tri_count;
+            }
             if (active && cast_local(S, bv, i, r, b)) hit = true;
         }
         return hit;
     }
     const int n = S.n_leaf;
     const RayInv ri = ray_inv(r);
-    wc.nodes += __popcll(am);                                  // root test
+    if (STATS) wc.nodes += __popcll(am);                       // root test
     const bool hr = active && node_hit(bv.a[1], bv.b[1], r, ri);
     const unsigned long long br = __ballot(hr);
     if (!br) return false;
@@ -233,8 +235,10 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         const unsigned long long m = __ballot(h);
         if (!m) return;
         const int ti = uni(bv.leaf[li]);                       // leaf instance: wave-uniform
-        wc.leaves += __popcll(m);
-        wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
+        if (STATS) {
+            wc.leaves += __popcll(m);
+            wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
+        }
         if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
         else if (h && cast_local(S, bv, ti, r, b)) {
             hit = true;
@@ -243,7 +247,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     };
     if (n == 1) { leaf(hr, 0); return hit; }
     // one copy of the leaf code for both children (keeps the kernel small)
-    wc.nodes += 2ull * __popcll(br);
+    if (STATS) wc.nodes += 2ull * __popcll(br);
     int k = 1;
     unsigned pending = 0;
     for (;;) {
@@ -256,7 +260,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             if (!__ballot(active)) break;                      // every lane occluded
         } else {
             const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
-            wc.nodes += 2ull * (__popcll(b0) + __popcll(b1));
+            if (STATS) wc.nodes += 2ull * (__popcll(b0) + __popcll(b1));
             if (b0) {
                 if (b1) pending |= 1u << (31 - __clz(c0));
                 k = c0;
@@ -284,12 +288,16 @@ __device__ __forceinline__ V4 phong(const DMat& m, V3 nrm, V4 incoming, V3 ray_d
     return (diffuse + specular) * incoming;
 }
 
-struct Frame {                // RayFrame (scene.cu:81-90)
+// RayFrame (scene.cu:81-90).  The top frame's hit point and normal are not kept in
+// registers: while the frame is being lit they equal at(ray, is_time) and is_norm
+// (the reference assigns them from exactly those, scene.cu:117-120), and a frame
+// resumed from the stack reads them from its saved copy.
+struct Frame {
     Ray ray;
-    V3 hit_pt, norm;
     V4 atten;
     int last_mat, type, depth, in_obj;
 };
+struct SavedFrame { Frame f; V3 hit_pt, norm; };   // suspended under its reflection child
 
 struct TraceParams {
     DCamera cam;
@@ -308,6 +316,10 @@ struct TraceParams {
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
 };
+
+// Opaque to the optimiser: values derived from x (64-bit output addresses) are formed
+// here instead of being hoisted to the group start and spilled across the trace.
+__device__ __forceinline__ void opaque(int& x) { asm volatile("" : "+v"(x)); }
 
 __device__ __forceinline__ void dbg(const TraceParams& P, bool me, int ev) {
     if (P.dbg_log && me) {
@@ -336,12 +348,15 @@ __device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
 // pixel's sample 0 and records the primary hit ids there.
 enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_WAIT_SHADOW = 4 };
 
-template <int NS>
+template <int NS, bool STATS>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
-                                           Ray r0, bool me, long out_p, WaveCounters& wc) {
-    Frame cur, stk[NS > 0 ? NS : 1];
+                                           Ray r0, bool me, int out_p, WaveCounters& wc) {
+    Frame cur;
+    SavedFrame stk[NS > 0 ? NS : 1];
     int top = -1, st = ST_DONE;
-    bool primary = true, pending_pop = false;
+    // bit 0: primary ray not yet answered; bit 1: pop after illumination (depth 0);
+    // bit 2: `cur` was resumed from stk[top] (hit point / normal live there)
+    int fl = 1;
     V4 acc = v4(0, 0, 0, 0);
     float is_time = INFINITY;                                   // the sample's shared Isect
     V3 is_norm = v3(0, 0, 0);
@@ -352,11 +367,15 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     float da = 1.0f, max_t = 0.0f;
     Ray q = r0;
     if (valid) {
-        cur.ray = r0; cur.hit_pt = v3(0, 0, 0); cur.norm = v3(0, 0, 0);
+        cur.ray = r0;
         cur.atten = v4(1.0f, 1.0f, 1.0f, 1.0f); cur.last_mat = -1;
         cur.type = F_NORMAL; cur.depth = P.depth; cur.in_obj = 0;
         top = 0; st = ST_ADVANCE;
     }
+    auto pop = [&]() {
+        top--;
+        if (top >= 0) { cur = stk[top].f; fl |= 4; }
+    };
     for (;;) {
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
@@ -384,7 +403,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                     st = ST_WAIT_SHADOW;
                 } else {
                     acc = acc + cur.atten * summed;                 // scene.cu:127
-                    if (pending_pop) { pending_pop = false; top--; if (top >= 0) cur = stk[top]; }
+                    if (fl & 2) { fl &= ~2; pop(); }
                     st = top < 0 ? ST_DONE : ST_ADVANCE;
                 }
                 continue;
@@ -399,19 +418,17 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             }
             const DMat& m = S.mats[is_mat];
             bool do_pop = false;
-            if (cur.type == F_REFLECT) {                           // scene.cu:129-148
+            if (cur.type == F_REFLECT) {                           // scene.cu:129-148 (frame's own hit)
                 cur.type = F_REFRACT;
                 if (m.reflective) {
                     dbg(P, me, 2);
-                    Frame c;
-                    c.type = F_NORMAL; c.last_mat = cur.last_mat; c.in_obj = cur.in_obj;
-                    c.atten = cur.atten * m.Kr;
-                    c.depth = cur.depth - 1;
-                    c.ray = make_ray(cur.hit_pt, reflect(cur.ray.d, normalized(cur.norm)));
-                    c.hit_pt = v3(0, 0, 0); c.norm = v3(0, 0, 0);
-                    stk[top] = cur;
+                    const V3 hp = at(cur.ray, is_time);
+                    stk[top].f = cur; stk[top].hit_pt = hp; stk[top].norm = is_norm;
                     top++;
-                    cur = c;
+                    cur.type = F_NORMAL;                           // the child: last_mat, in_obj inherited
+                    cur.atten = cur.atten * m.Kr;
+                    cur.depth = cur.depth - 1;
+                    cur.ray = make_ray(hp, reflect(cur.ray.d, normalized(is_norm)));
                 }
             } else if (m.refractive) {                            // F_REFRACT (scene.cu:149-184)
                 dbg(P, me, 3);
@@ -419,14 +436,17 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 float n1, n2;
                 if (cur.in_obj) { n1 = S.mats[cur.last_mat].eta; n2 = 1.0f; }
                 else { n1 = 1.0f; n2 = S.mats[cur.last_mat].eta; }
+                V3 hp, nn;
+                if (fl & 4) { hp = stk[top].hit_pt; nn = stk[top].norm; }
+                else { hp = at(cur.ray, is_time); nn = is_norm; }
                 bool tir;
-                V3 rd = refract(cur.ray.d, normalized(cur.norm), n1, n2, tir);
+                V3 rd = refract(cur.ray.d, normalized(nn), n1, n2, tir);
                 if (tir) do_pop = true;
-                else { cur.ray = make_ray(cur.hit_pt, rd); cur.in_obj = !cur.in_obj; cur.depth--; }
+                else { cur.ray = make_ray(hp, rd); cur.in_obj = !cur.in_obj; cur.depth--; }
             } else {
                 do_pop = true;
             }
-            if (do_pop) { top--; if (top >= 0) cur = stk[top]; else st = ST_DONE; }
+            if (do_pop) { pop(); if (top < 0) st = ST_DONE; }
         }
         // ---- the wave-collective closest-hit query ----
         const bool need = (st == ST_WAIT_NORMAL || st == ST_WAIT_SHADOW);
@@ -435,26 +455,29 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
         float occl = -1.0f;
         if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
-        const bool hit = closest_hit(S, bv, need, q, b, wc, occl);
+        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl);
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
         if (hit) hn = hit_normal(S, bv, b, hmat);
         if (st == ST_WAIT_NORMAL) {
-            if (primary) {
-                primary = false;
+            if (fl & 1) {
+                fl &= ~1;
                 if (out_p >= 0) {
-                    if (P.hit_inst) P.hit_inst[out_p] = hit ? b.inst : -1;
-                    if (P.hit_tri) P.hit_tri[out_p] = hit ? b.tri : -1;
+                    int op = out_p;
+                    opaque(op);
+                    if (P.hit_inst) P.hit_inst[op] = hit ? b.inst : -1;
+                    if (P.hit_tri) P.hit_tri[op] = hit ? b.tri : -1;
                 }
             }
             if (!hit) {                                            // scene.cu:124-126
                 is_time = INFINITY;
-                top--;
-                if (top >= 0) { cur = stk[top]; st = ST_ADVANCE; } else st = ST_DONE;
+                pop();
+                st = top >= 0 ? ST_ADVANCE : ST_DONE;
                 continue;
             }
             is_time = b.time; is_norm = hn; is_mat = hmat;
+            fl &= ~4;                                              // hit point / normal = at(ray, is_time), is_norm
             if (cur.depth > 0) {                                   // scene.cu:109-121
                 if (cur.in_obj) {
                     const V4 kt = S.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
@@ -462,11 +485,9 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                                                pow_ref(is_time, kt.z), pow_ref(is_time, kt.w));
                 }
                 cur.type = F_REFLECT;
-                cur.hit_pt = at(cur.ray, is_time);
                 cur.last_mat = is_mat;
-                cur.norm = is_norm;
             } else {
-                pending_pop = true;                                // popped after illumination (frame still needed)
+                fl |= 2;                                           // popped after illumination (frame still needed)
             }
             const DMat& m = S.mats[is_mat];                        // org_light (phong.cu:36-39)
             summed = m.Ke + m.Ka * P.ambience;
@@ -511,7 +532,12 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // A group = `px_per_wave` pixels x `lanes_per_px` samples; lane (pixel p, sub s)
 // traces samples k = round*L + s and the group leader sums the clamped sample
 // radiance in k order (build-defined spp extension).
-template <int NS, bool LDS>
+// MODE bit 0 (MULTI): spp > 64 -- several rounds of samples per lane (the per-pixel sums
+// then stay live across rounds, which the common single-round kernel avoids).
+// MODE bit 1 (STATS): exact work counters.  The divergent state machine keeps 64-bit
+// counters in VGPRs, so frames without statistics use a kernel without them.
+constexpr int M_MULTI = 1, M_STATS = 2;
+template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     BvhRefs bv;
@@ -532,7 +558,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
-    const int rounds = (P.spp + L - 1) / L;
+    constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0;
+    const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
     // a wave drains its own queue (c = block % NQ, i.e. one per XCD dispatch slot) then the
@@ -558,7 +585,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
         const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
         const int py = P.row0 + pr * P.row_step;
-        const long p = P.compact ? (long)pr * P.W + px : (long)py * P.W + px;
+        const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
         const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         for (int rd = 0; rd < rounds; rd++) {
@@ -569,7 +596,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
                 float2 o = P.spp_off[k];
                 r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
             }
-            V4 c = trace_sample<NS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? p : -1, wc);
+            V4 c = trace_sample<NS, STATS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc);
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
                 V4 v = shfl4(c, base + s);
                 if (sub == 0 && rd * L + s < P.spp) {
@@ -580,6 +607,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             }
         }
         if (valid && sub == 0) {
+            int p = pix_index;
+            opaque(p);                                         // address math stays here, not live across the trace
             const float inv = (float)P.spp;
             const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
             // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
@@ -589,7 +618,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
     }
-    if (P.stats && lane == 0) {
+    if (STATS && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
         if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
         if (wc.leaves) atomicAdd(&P.stats[2], wc.leaves);
@@ -641,7 +670,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams
         Ray r{v3(0, 0, 0), v3(0, 0, 1)};
         if (valid) { float2 o = P.spp_off[sub]; r = camera_at(P.cam, (float)px + o.x, (float)py + o.y); }
         Best b; b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0; b.v = 0;
-        bool h = closest_hit<NOLEAF>(S, bv, valid, r, b, wc);
+        bool h = closest_hit<NOLEAF, true>(S, bv, valid, r, b, wc);
         if (valid) out[((size_t)pr * P.W + px) * P.lanes_per_px + sub] = make_float4(h ? b.time : -1.0f, __int_as_float(b.inst), b.u, b.v);
     }
     if (P.stats && lane == 0) {
@@ -981,10 +1010,16 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
     const void* fn;
-    if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true> : ns <= 2 ? (const void*)trace_kernel<2, true>
-                                                                       : (const void*)trace_kernel<MAX_FRAMES - 1, true>;
-    else fn = ns <= 0 ? (const void*)trace_kernel<0, false> : ns <= 2 ? (const void*)trace_kernel<2, false>
-                                                             : (const void*)trace_kernel<MAX_FRAMES - 1, false>;
+    const int mode = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
+    constexpr int NG = MAX_FRAMES - 1;                     // generic frame-stack depth
+    static const void* const generic[2][4] = {
+        {(const void*)trace_kernel<NG, false, 0>, (const void*)trace_kernel<NG, false, 1>,
+         (const void*)trace_kernel<NG, false, 2>, (const void*)trace_kernel<NG, false, 3>},
+        {(const void*)trace_kernel<NG, true, 0>, (const void*)trace_kernel<NG, true, 1>,
+         (const void*)trace_kernel<NG, true, 2>, (const void*)trace_kernel<NG, true, 3>}};
+    if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
+    else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
+    else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
     const size_t shm = use_lds ? lds : 0;
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
@@ -1263,6 +1298,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     int r;
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
+    if ((size_t)s->h.cam.W * s->h.cam.H > (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame larger than 2^31 pixels");
     if ((r = ensure_spp(s, o->spp)) != RT_OK) return r;
     hipStream_t st = o->stream ? (hipStream_t)o->stream : s->stream;
     const bool timed = stats != nullptr;

@@ -1,0 +1,63 @@
+"""Turn a tools/profile.sh run into profiles/pmc_traffic.json (HBM bytes per trace launch)
+and a short markdown summary.
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived memory-side (TCC EA) counters in KiB.
+Per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half of the bytes of wide
+coalesced streaming reads, so the read side is doubled; WRITE_SIZE is calibrated here
+against the known frame store (4 B per pixel of RGBA8) -- see `write_calibration`.
+
+Usage: python tools/pmc_traffic.py PROFILE_DIR KEY W ROWS [OUT_JSON]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(root, counter, pat="trace_kernel"):
+    vals = collections.defaultdict(float)
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if pat in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+    v = list(vals.values())
+    return (sum(v) / len(v), len(v)) if v else (None, 0)
+
+
+def kernel_stats(root, pat="trace_kernel"):
+    for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if pat in r["Name"]:
+                return {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                        "max_ns": float(r["MaxNs"])}
+    return None
+
+
+def main():
+    root, key, W, rows = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
+    fetch_kib, nf = per_dispatch(root, "FETCH_SIZE")
+    write_kib, nw = per_dispatch(root, "WRITE_SIZE")
+    if fetch_kib is None or write_kib is None:
+        sys.exit("no FETCH_SIZE/WRITE_SIZE rows for trace_kernel under " + root)
+    frame_bytes = 4 * W * rows
+    rd = 2.0 * fetch_kib * 1024.0                      # gfx950: FETCH_SIZE counts half of wide reads
+    wr = write_kib * 1024.0
+    entry = {
+        "hbm_bytes_per_launch": int(rd + wr),
+        "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
+        "raw": {"FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib, "dispatches": [nf, nw]},
+        "write_calibration": {"frame_store_bytes": frame_bytes, "write_over_frame": wr / frame_bytes},
+        "kernel_trace": kernel_stats(root),
+        "source": os.path.relpath(root),
+    }
+    db = json.load(open(out)) if os.path.exists(out) else {}
+    db[key] = entry
+    json.dump(db, open(out, "w"), indent=1, sort_keys=True)
+    print(json.dumps({key: entry}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
