@@ -24,6 +24,7 @@ import torch  # first: the HIP runtime torch loads is the one librt_amd.so binds
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
 import rtamd  # noqa: E402
+import rtamd.dist as rtdist  # noqa: E402
 
 METRIC = "Mrays/sec (primary+secondary) + frame ms, 1080p world8_stress, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
@@ -41,29 +42,43 @@ def parse():
     p.add_argument("--spp", type=int, default=8)
     p.add_argument("--brute", action="store_true", help="reference -r: no BVH")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample-rows", type=int, default=2, help="CPU baseline renders rows y %% k == 0")
+    p.add_argument("--cpu-sample-rows", type=int, default=1, help="CPU baseline renders rows y %% k == 0")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
 
 def cpu_baseline(args, scene_path):
     """The reference's CPU path (src/raytracer.cc semantics, restated in oracle/) on a
-    bounded sample of the same workload, 1 thread — the reference's CPU path is serial."""
+    bounded sample of the same workload, 1 thread -- the reference's CPU path is serial
+    (SURVEY §8d).  Beside it, the GPU-semantics restatement on the host cores this job
+    may use (apples-to-apples work, OpenMP-style row split)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import Oracle
     orc = Oracle()
     s = orc.load(scene_path, args.width, args.height)
     k = max(1, args.cpu_sample_rows)
+    bvh = 0 if args.brute else 1
     t = time.perf_counter()
-    fr = orc.render(s, semantics=1, use_bvh=0 if args.brute else 1, spp=1, row0=0, row_step=k, nthreads=1, want=())
+    fr = orc.render(s, semantics=1, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=1, want=())
     dt = time.perf_counter() - t
     rays = int(fr["stats"][0])
     rows = len(range(0, args.height, k))
+    nthr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    t = time.perf_counter()
+    fg = orc.render(s, semantics=0, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=nthr, want=())
+    dg = time.perf_counter() - t
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        cpu_model = "unknown"
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
         "sample": "%s %dx%d rows y%%%d==0 (%d rows), spp=1, CPU-path semantics of src/raytracer.cc "
                   "(oracle restatement), 1 thread; %.1f s, %d rays; extrapolated frame at %d spp: %.0f ms"
                   % (args.scene, args.width, args.height, k, rows, dt, rays, args.spp, dt * k * args.spp * 1e3),
+        "gpu_semantics_all_cores": {"value": int(fg["stats"][0]) / dg / 1e6, "unit": "Mrays/s", "cores": nthr,
+                                    "seconds": round(dg, 2)},
+        "cpu_model": cpu_model,
     }
 
 
@@ -83,25 +98,16 @@ def main():
     scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")
     scene = rtamd.Scene.load_json(scene_path, args.width, args.height)
     W, H = scene.width, scene.height
-    rows_per = (H + world - 1) // world                 # padded slice height (equal RCCL message sizes)
-    my_rows = len(range(rank, H, world))
-    part = torch.zeros((rows_per, W), dtype=torch.int32, device="cuda")
+    my_rows = len(rtdist.rows_of(rank, world, H))
+    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist)
+    part = fb.part
     stream = torch.cuda.current_stream()
-    gathered = [torch.empty_like(part) for _ in range(world)] if (world > 1 and rank == 0) else None
-    frame = torch.empty((H, W), dtype=torch.int32, device="cuda") if rank == 0 else None
     use_bvh = not args.brute
 
     def step(timing):
         scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
                             compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, timing=timing)
-        if world > 1:
-            dist.gather(part, gathered, dst=0)
-            if rank == 0:
-                for r in range(world):                  # un-permute row-cyclic slices
-                    n = len(range(r, H, world))
-                    frame[r::world] = gathered[r][:n]
-        elif rank == 0:
-            frame.copy_(part[:H])
+        fb.gather()
 
     # per-frame work counters (deterministic): one untimed counted render of this rank's rows
     st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
@@ -127,7 +133,7 @@ def main():
     for _ in range(max(1, args.steps // 2)):
         step(False)
         if rank == 0:
-            host = frame.cpu()
+            host = fb.frame.cpu()
     torch.cuda.synchronize()
     rb_ms = (time.perf_counter() - t2) / max(1, args.steps // 2) * 1e3
 
