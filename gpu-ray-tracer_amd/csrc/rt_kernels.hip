@@ -76,6 +76,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
+    int ident_all;            // every instance and mesh rotation is the identity (cube worlds)
 };
 
 // Wave-uniform read-only records in global memory are read through the
@@ -153,17 +154,42 @@ __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv,
 // Hitable::hit (hitable.cu:29-38) -> Trimesh::hit_local (trimesh.cu:11-19) with a
 // wave-uniform instance; times are rescaled here exactly as in the reference
 // (later comparisons depend on them); the normal is formed after traversal.
-__device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b) {
+// With identity rotations everywhere (S.ident_all), the direction half of cast_local's
+// two pose changes depends on the ray only: it is computed once per query by the same
+// operations (qrot_identity, len, the Ray ctor's normalisation), so every leaf sees
+// the same bits it would compute itself; only the origin chain is per leaf.
+struct DirPre { V3 mrd; float scale, dir_len; };
+__device__ __forceinline__ DirPre dir_pre(V3 d) {
+    DirPre p;
+    const V3 ld = qrot_identity(d);                          // Entity::vec_to_local, identity pose
+    p.dir_len = len(ld);
+    const V3 lrd = normalized(ld);                           // Ray ctor (geometry.h:216)
+    const V3 md = qrot_identity(lrd);                        // HitHandle::get_local_ray, identity mesh pose
+    p.scale = len(md);
+    p.mrd = normalized(md);
+    return p;
+}
+
+__device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b,
+                                           const DirPre& pre) {
     int mesh_id;
     const Pose ip = inst_pose(S, bv, ti, mesh_id);
     mesh_id = uni(mesh_id);
     const DMesh mesh = ldc(S.meshes, mesh_id);
-    V3 ld = vec_to_local(ip, r.d);
-    float dir_len = len(ld);
-    Ray lr = make_ray(point_to_local(ip, r.o), ld);
-    V3 md = vec_to_local(mesh.pose, lr.d);                   // HitHandle::get_local_ray
-    float scale = len(md);
-    Ray mr = make_ray(point_to_local(mesh.pose, lr.o), md);
+    float dir_len, scale;
+    Ray mr;
+    if (S.ident_all) {
+        dir_len = pre.dir_len; scale = pre.scale;
+        mr.o = qrot_identity(qrot_identity(r.o - ip.p) - mesh.pose.p);
+        mr.d = pre.mrd;
+    } else {
+        V3 ld = vec_to_local(ip, r.d);
+        dir_len = len(ld);
+        Ray lr = make_ray(point_to_local(ip, r.o), ld);
+        V3 md = vec_to_local(mesh.pose, lr.d);               // HitHandle::get_local_ray
+        scale = len(md);
+        mr = make_ray(point_to_local(mesh.pose, lr.o), md);
+    }
     int best = -1;
     float bu = 0.0f, bv_ = 0.0f, t_best = b.time;
     for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
@@ -216,12 +242,14 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     if (STATS) wc.rays += __popcll(am);
     bool hit = false;
     if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
+        DirPre pre{};
+        if (S.ident_all) pre = dir_pre(r.d);
         for (int i = 0; i < S.n_inst; i++) {
             if (STATS) {
                 wc.leaves += __popcll(am);
                 wc.tris += (unsigned long long)__popcll(am) * ldc(S.meshes, uni(__float_as_int(bv.inst[i].w) & 0x7fffffff)).tri_count;
             }
-            if (active && cast_local(S, bv, i, r, b)) hit = true;
+            if (active && cast_local(S, bv, i, r, b, pre)) hit = true;
         }
         return hit;
     }
@@ -231,6 +259,8 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     const bool hr = active && node_hit(bv.a[1], bv.b[1], r, ri);
     const unsigned long long br = __ballot(hr);
     if (!br) return false;
+    DirPre pre{};
+    if (S.ident_all) pre = dir_pre(r.d);
     auto leaf = [&](bool h, int li) {
         const unsigned long long m = __ballot(h);
         if (!m) return;
@@ -240,7 +270,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
         }
         if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
-        else if (h && cast_local(S, bv, ti, r, b)) {
+        else if (h && cast_local(S, bv, ti, r, b, pre)) {
             hit = true;
             if (b.time <= occl_t) active = false;             // occluded: this lane is done
         }
@@ -971,6 +1001,9 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     v.node_a = s->d_node_a; v.node_b = s->d_node_b; v.leaf_inst = s->d_leaf; v.inst4 = s->d_inst4;
     v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
+    v.ident_all = 1;
+    for (const auto& i : s->h.d_insts) v.ident_all &= i.pose.identity ? 1 : 0;
+    for (const auto& m : s->h.d_meshes) v.ident_all &= m.pose.identity ? 1 : 0;
     return v;
 }
 

@@ -16,20 +16,29 @@ import os
 import sys
 
 
-def per_dispatch(root, counter, pat="trace_kernel"):
+def is_timed_trace(name):
+    """The frame kernel bench.py times: trace_kernel<NS, LDS, MODE> without the STATS bit
+    (the single counted frame bench.py renders first uses MODE 2/3)."""
+    if "trace_kernel<" not in name:
+        return False
+    mode = name.split("trace_kernel<", 1)[1].split(">", 1)[0].split(",")[-1].strip()
+    return mode in ("0", "1")
+
+
+def per_dispatch(root, counter, sel=is_timed_trace):
     vals = collections.defaultdict(float)
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if pat in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if sel(r["Kernel_Name"]) and r["Counter_Name"] == counter:
                 vals[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     v = list(vals.values())
     return (sum(v) / len(v), len(v)) if v else (None, 0)
 
 
-def kernel_stats(root, pat="trace_kernel"):
+def kernel_stats(root, sel=is_timed_trace):
     for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if pat in r["Name"]:
+            if sel(r["Name"]):
                 return {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                         "max_ns": float(r["MaxNs"])}
     return None
@@ -40,6 +49,8 @@ def main():
     out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
     fetch_kib, nf = per_dispatch(root, "FETCH_SIZE")
     write_kib, nw = per_dispatch(root, "WRITE_SIZE")
+    rdreq, _ = per_dispatch(root, "TCC_EA0_RDREQ_sum")
+    wrreq, _ = per_dispatch(root, "TCC_EA0_WRREQ_sum")
     if fetch_kib is None or write_kib is None:
         sys.exit("no FETCH_SIZE/WRITE_SIZE rows for trace_kernel under " + root)
     frame_bytes = 4 * W * rows
@@ -48,7 +59,8 @@ def main():
     entry = {
         "hbm_bytes_per_launch": int(rd + wr),
         "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
-        "raw": {"FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib, "dispatches": [nf, nw]},
+        "raw": {"FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib, "dispatches": [nf, nw],
+                "TCC_EA0_RDREQ": rdreq, "TCC_EA0_WRREQ": wrreq},
         "write_calibration": {"frame_store_bytes": frame_bytes, "write_over_frame": wr / frame_bytes},
         "kernel_trace": kernel_stats(root),
         "source": os.path.relpath(root),
