@@ -77,6 +77,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
     int ident_all;            // every instance and mesh rotation is the identity (cube worlds)
+    float prune_abs;          // distance-pruning slack M0 (< 0: pruning off), see closest_hit
 };
 
 // Wave-uniform read-only records in global memory are read through the
@@ -133,6 +134,13 @@ __device__ __forceinline__ bool node_hit(float4 A, float2 B, const Ray& r, const
 #else
     return box_hit(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r);
 #endif
+}
+
+// node_hit + a lower bound of the box entry distance (for distance pruning)
+__device__ __forceinline__ bool node_hit_t(float4 A, float2 B, const Ray& r, const RayInv& ri, float& tlo) {
+    tlo = -INFINITY;
+    if (!(A.x <= A.w)) return false;
+    return box_hit_ft(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r, ri, tlo);
 }
 
 struct Best { float time; int inst, tri; float u, v; };     // closest accepted triangle so far
@@ -234,9 +242,27 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 // is < that time up to the instance/mesh rescaling, |scale - 1| <= 4u), so
 // Light::attenuate returns 0 either way (light.cu:39-45).  Counters then count
 // the work done, so it is only used when statistics are not requested.
+//
+// Distance pruning (frames without statistics, S.prune_abs >= 0): a lane skips a
+// subtree/leaf whose box entry bound tlo exceeds cut = c + M, c = min(b.time, lim).
+// Exact: the subtree's leaves are processed later with b.time <= c, and none of
+// their triangles can be accepted.  An accepted local time t satisfies
+// t >= tmin_box - M: the hit point is within 1e-5 x (triangle size) of its triangle
+// (the barycentric-sum tolerance, geometry.h:281-286), the triangle is inside the
+// box when every pose is a pure translation and mesh offsets are zero (the host
+// checks), the pose chains round by O(u |coords|) and tlo <= tmin.  M = prune_abs
+// (1e-4 x mesh size + 2^-14 x scene radius) + 2^-14 c covers these with a wide
+// factor.  `lim` = max_t for shadow segments: hits beyond it never change
+// Light::attenuate (light.cu:35-58).
 template <bool NOLEAF, bool STATS>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
-                                            Best& b, WaveCounters& wc, float occl_t = -1.0f) {
+                                            Best& b, WaveCounters& wc, float occl_t = -1.0f,
+                                            float lim = INFINITY) {
+    const bool prune = !STATS && S.prune_abs >= 0.0f;
+    auto cut = [&]() {
+        const float c = fminf(b.time, lim);
+        return c + (S.prune_abs + 0x1p-14f * c);
+    };
     bool active = active_in;
     const unsigned long long am = __ballot(active);
     if (STATS) wc.rays += __popcll(am);
@@ -282,11 +308,22 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     unsigned pending = 0;
     for (;;) {
         const int c0 = 2 * k;
-        const bool h0 = active && node_hit(bv.a[c0], bv.b[c0], r, ri);
-        const bool h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r, ri);
+        bool h0, h1;
+        float t1 = -INFINITY;
+        if (prune) {
+            float t0;
+            h0 = active && node_hit_t(bv.a[c0], bv.b[c0], r, ri, t0);
+            h1 = active && node_hit_t(bv.a[c0 + 1], bv.b[c0 + 1], r, ri, t1);
+            const float ct = cut();
+            h0 = h0 && !(t0 > ct);
+            h1 = h1 && !(t1 > ct);
+        } else {
+            h0 = active && node_hit(bv.a[c0], bv.b[c0], r, ri);
+            h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r, ri);
+        }
         if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
 #pragma nounroll
-            for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : h1, c0 + c - n);
+            for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : (h1 && !(prune && t1 > cut())), c0 + c - n);
             if (!__ballot(active)) break;                      // every lane occluded
         } else {
             const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
@@ -485,7 +522,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
         float occl = -1.0f;
         if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
-        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl);
+        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl,
+                                                   st == ST_WAIT_SHADOW ? max_t : INFINITY);
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
@@ -1004,6 +1042,18 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     v.ident_all = 1;
     for (const auto& i : s->h.d_insts) v.ident_all &= i.pose.identity ? 1 : 0;
     for (const auto& m : s->h.d_meshes) v.ident_all &= m.pose.identity ? 1 : 0;
+    // Distance pruning (closest_hit): boxes provably contain their triangles only for
+    // pure translations with zero mesh offsets (the BVH boxes ignore the mesh pose,
+    // raytracer.cu:54-89).  Slack: 1e-4 x mesh size + 2^-14 x scene radius.
+    bool prune_ok = v.ident_all != 0;
+    float vmax = 0.0f, pmax = 0.0f;
+    for (const auto& m : s->h.d_meshes) prune_ok = prune_ok && m.pose.p.x == 0 && m.pose.p.y == 0 && m.pose.p.z == 0;
+    auto amax = [](rtm::V3 a) { return std::max(std::fabs(a.x), std::max(std::fabs(a.y), std::fabs(a.z))); };
+    for (const auto& t : s->h.d_tris) vmax = std::max(vmax, std::max(amax(t.a), std::max(amax(t.b), amax(t.c))));
+    for (const auto& i : s->h.d_insts) pmax = std::max(pmax, amax(i.pose.p));
+    const float radius = pmax + vmax + amax(s->h.d_cam.pos) + 1.0f;
+    prune_ok = prune_ok && std::isfinite(radius);
+    v.prune_abs = prune_ok ? 4e-4f * vmax + 0x1p-14f * radius : -1.0f;
     return v;
 }
 

@@ -263,6 +263,21 @@ RT_HD bool box_hit_f(V3 mn, V3 mx, const Ray& r, const RayInv& ri) {
     return box_hit(mn, mx, r);                                           // near a tie: exact
 }
 
+// box_hit_f that also returns tlo, a lower bound of the exact slab entry distance
+// (|tmin_f - tmin| <= E, see above); -inf when the exact test decided.
+RT_HD bool box_hit_ft(V3 mn, V3 mx, const Ray& r, const RayInv& ri, float& tlo) {
+    tlo = -INFINITY;
+    if (ri.exact) return box_hit(mn, mx, r);
+    float tmin = -INFINITY, tmax = INFINITY, m = 0.0f;
+    slab_axis_f(mn.x, mx.x, r.o.x, r.d.x, ri.ix, tmin, tmax, m);
+    slab_axis_f(mn.y, mx.y, r.o.y, r.d.y, ri.iy, tmin, tmax, m);
+    slab_axis_f(mn.z, mx.z, r.o.z, r.d.z, ri.iz, tmin, tmax, m);
+    const float E = m * FILT_BOX + FILT_ABS;
+    if (tmin - tmax > 2.0f * E || tmax + E < THRESH) return false;
+    if (tmin + 2.0f * E <= tmax && tmax - E >= THRESH) { tlo = tmin - 2.0f * E; return true; }
+    return box_hit(mn, mx, r);
+}
+
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }

@@ -127,10 +127,13 @@ def test_empty_scene_renders_black(gpu, tmp_path):
     assert (fr["rgba"] == 0).all() and (fr["hit_inst"] == -1).all()
 
 
-@pytest.mark.parametrize("scene,spp", [("world8_stress", 4), ("world16", 1), ("world1", 2)])
+@pytest.mark.parametrize("scene,spp", [("world8_stress", 4), ("world16", 1), ("world1", 2), ("world8", 2),
+                                       ("config", 2)])
 def test_occlusion_early_exit_is_exact(gpu, oracle, scene, spp):
-    """Frames rendered without statistics use the shadow-ray occlusion early exit (all-opaque
-    scenes); they must equal the counted (full closest-hit) frames and the oracle."""
+    """Frames rendered without statistics use the fast kernel: shadow-ray occlusion early
+    exit (all-opaque scenes) and distance pruning of subtrees beyond the current closest
+    hit.  They must equal the counted (full closest-hit, reference traversal) frames bit
+    for bit, and the oracle."""
     s = gpu.Scene.load_json(scene_path(scene), 240, 160)
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     fast = s.render(spp=spp, want=want, stats=False)
@@ -139,3 +142,19 @@ def test_occlusion_early_exit_is_exact(gpu, oracle, scene, spp):
         assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
     o = oracle.render(oracle.load(scene_path(scene), 240, 160), spp=spp, nthreads=8)
     check_frame(fast, o, spp)
+
+
+def test_fast_kernel_exact_close_camera(gpu, oracle):
+    """Distance pruning with the camera inside the cube field (rays start next to boxes,
+    many near-ties between overlapping leaves)."""
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 200, 150)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    _, rot = s.camera()
+    # the cubes fill x, z in [-4, 3], y in [0, 11]; the camera looks down at ~58 degrees
+    for pos in ([0.5, 14.0, -0.5], [0.37, 6.21, -1.13], [-3.9, 10.5, 2.9], [0.0, 3.0, -6.5]):
+        s.set_camera(pos, rot)
+        fast = s.render(spp=2, want=want, stats=False)
+        full = s.render(spp=2, want=want, stats=True)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
+        assert (full["hit_inst"] >= 0).mean() > 0.05, pos
