@@ -71,8 +71,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DInst* __restrict__ insts;
     const DMat* __restrict__ mats;
     const DLight* __restrict__ lights;
-    const float4* node_a;     // BVH, heap order, SoA (written by bvh_build_kernel)
-    const float2* node_b;
+    const float4* node_pair;  // BVH child pairs, heap order (written by bvh_build_kernel), see BvhRefs
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
@@ -113,12 +112,15 @@ __device__ __forceinline__ bool tri_accept(const DTri& T, const Ray& r, float be
     return false;
 }
 
-// BVH node (heap index k) and instance records as the trace kernel reads them:
-// from LDS (staged once per persistent block) or, for scenes too large for LDS,
-// straight from global memory.  Degenerate boxes are stored as min=+inf, max=-inf.
+// BVH nodes and instance records as the trace kernel reads them: from LDS (staged
+// once per persistent block) or, for scenes too large for LDS, from global memory.
+// Nodes are stored by child pair: pair k holds heap nodes 2k (.x lanes) and 2k+1 (.y
+// lanes) as three float4 = (mnx, mnx' , mny, mny'), (mnz, mnz', mxx, mxx'),
+// (mxy, mxy', mxz, mxz'), so one pair test is three 16-B broadcast reads and packed
+// (v_pk_*) slab arithmetic.  Pair 0 = (unused node 0, root).  Degenerate boxes are
+// stored as min=+inf, max=-inf.
 struct BvhRefs {
-    const float4* a;        // [2n] (mnx, mny, mnz, mxx)
-    const float2* b;        // [2n] (mxy, mxz)
+    const float4* pair;     // [3n]
     const int* leaf;        // [n]  instance of leaf node n+i (bvh.cu ordering[])
     const float4* inst;     // [n_inst] (px, py, pz, mesh | 0x80000000 if the pose is not identity)
 };
@@ -127,24 +129,64 @@ struct BvhRefs {
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
 
-__device__ __forceinline__ bool node_hit(float4 A, float2 B, const Ray& r, const RayInv& ri) {
-    if (!(A.x <= A.w)) return false;                          // !nondegenerate (bounding_box.cu:63-65)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
+__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return f2{fminf(a.x, b.x), fminf(a.y, b.y)}; }
+__device__ __forceinline__ f2 vmax(f2 a, f2 b) { return f2{fmaxf(a.x, b.x), fmaxf(a.y, b.y)}; }
+
+// BoundingBox::intersects (bounding_box.cu:62-104) for both children of pair k.
+// Filtered like box_hit_f (rt_math.h), with the bound taken from the slab results
+// themselves: every quotient q' = fl(e * fl(1/d)) is within 3.01u |q| of the
+// reference's fl(e / d), min and max keep a relative bound (|max a' - max a| <=
+// 3.03u max(|a|, |a'|)), so |lo' - lo| <= 6.1u |lo'| and the same for hi; the test
+// uses 16u plus an absolute floor.  Zero direction components are skipped through
+// the RayInv bias (see ray_inv); rays with a non-finite reciprocal (ri.exact) and
+// boxes near a tie take the exact reference test.
+// tlo (pruning) is a lower bound of the exact entry distance, -inf if undecided.
+__device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
+                                         bool& h0, bool& h1, float& t0, float& t1) {
+    const float4 A = np[3 * k], B = np[3 * k + 1], C = np[3 * k + 2];
+    const bool nd0 = A.x <= B.z, nd1 = A.y <= B.w;            // nondegenerate (bounding_box.cu:63-65)
+    t0 = -INFINITY; t1 = -INFINITY;
+    auto exact = [&](int c) {
+        return c == 0 ? box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) : box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r);
+    };
 #if RT_FILTERED
-    return box_hit_f(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r, ri);
+    const f2 mnx{A.x, A.y}, mny{A.z, A.w}, mnz{B.x, B.y}, mxx{B.z, B.w}, mxy{C.x, C.y}, mxz{C.z, C.w};
+    const f2 ix = splat(ri.ix), iy = splat(ri.iy), iz = splat(ri.iz);
+    const f2 bx = splat(ri.bx), by = splat(ri.by), bz = splat(ri.bz);
+    const f2 qx0 = __builtin_elementwise_fma(mnx - splat(r.o.x), ix, -bx), qx1 = __builtin_elementwise_fma(mxx - splat(r.o.x), ix, bx);
+    const f2 qy0 = __builtin_elementwise_fma(mny - splat(r.o.y), iy, -by), qy1 = __builtin_elementwise_fma(mxy - splat(r.o.y), iy, by);
+    const f2 qz0 = __builtin_elementwise_fma(mnz - splat(r.o.z), iz, -bz), qz1 = __builtin_elementwise_fma(mxz - splat(r.o.z), iz, bz);
+    const f2 lo = vmax(vmax(vmin(qx0, qx1), vmin(qy0, qy1)), vmin(qz0, qz1));
+    const f2 hi = vmin(vmin(vmax(qx0, qx1), vmax(qy0, qy1)), vmax(qz0, qz1));
+    const f2 el{fabsf(lo.x) * FILT_BOX + FILT_ABS, fabsf(lo.y) * FILT_BOX + FILT_ABS};
+    const f2 eh{fabsf(hi.x) * FILT_BOX + FILT_ABS, fabsf(hi.y) * FILT_BOX + FILT_ABS};
+    const f2 sep = (lo + el) - (hi - eh);                     // > 0 certainly lo > hi; <= 0 certainly lo <= hi
+    const f2 gap = (lo - el) - (hi + eh);
+    const f2 hlo = hi - eh, hhi = hi + eh;
+    const bool fx = active && !ri.exact;
+    // certainly a miss / certainly a hit (exact reference result known)
+    const bool m0 = !nd0 || (fx && (gap.x > 0.0f || hhi.x < THRESH));
+    const bool m1 = !nd1 || (fx && (gap.y > 0.0f || hhi.y < THRESH));
+    const bool c0 = fx && !m0 && sep.x <= 0.0f && hlo.x >= THRESH;
+    const bool c1 = fx && !m1 && sep.y <= 0.0f && hlo.y >= THRESH;
+    h0 = c0; h1 = c1;
+    if (c0) t0 = lo.x - el.x;
+    if (c1) t1 = lo.y - el.y;
+    if (active && !m0 && !c0) h0 = exact(0);
+    if (active && !m1 && !c1) h1 = exact(1);
 #else
-    return box_hit(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r);
+    h0 = active && nd0 && exact(0);
+    h1 = active && nd1 && exact(1);
 #endif
 }
 
-// node_hit + a lower bound of the box entry distance (for distance pruning)
-__device__ __forceinline__ bool node_hit_t(float4 A, float2 B, const Ray& r, const RayInv& ri, float& tlo) {
-    tlo = -INFINITY;
-    if (!(A.x <= A.w)) return false;
-    return box_hit_ft(v3(A.x, A.y, A.z), v3(A.w, B.x, B.y), r, ri, tlo);
-}
-
 struct Best { float time; int inst, tri; float u, v; };     // closest accepted triangle so far
-struct WaveCounters { unsigned long long rays, nodes, leaves, tris; };   // wave-uniform (SGPRs)
+// Per-lane work counters (rays/nodes/leaves/triangle tests, the reference's units) plus
+// wave-level step counts for the profiling experiment (query iterations, child-pair
+// steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 
@@ -265,7 +307,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     };
     bool active = active_in;
     const unsigned long long am = __ballot(active);
-    if (STATS) wc.rays += __popcll(am);
+    if (STATS) { wc.rays += __popcll(am); wc.wq++; }
     bool hit = false;
     if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
         DirPre pre{};
@@ -282,7 +324,9 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     const int n = S.n_leaf;
     const RayInv ri = ray_inv(r);
     if (STATS) wc.nodes += __popcll(am);                       // root test
-    const bool hr = active && node_hit(bv.a[1], bv.b[1], r, ri);
+    bool hr, hdummy;
+    float tdummy, troot;
+    pair_hit(bv.pair, 0, r, ri, active, hdummy, hr, tdummy, troot);   // pair 0 = (unused, root)
     const unsigned long long br = __ballot(hr);
     if (!br) return false;
     DirPre pre{};
@@ -292,8 +336,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         if (!m) return;
         const int ti = uni(bv.leaf[li]);                       // leaf instance: wave-uniform
         if (STATS) {
+            const int tc = ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
             wc.leaves += __popcll(m);
-            wc.tris += (unsigned long long)__popcll(m) * ldc(S.meshes, uni(__float_as_int(bv.inst[ti].w) & 0x7fffffff)).tri_count;
+            wc.tris += (unsigned long long)__popcll(m) * tc;
+            wc.wleaf++;
+            wc.wtri += tc;
         }
         if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
         else if (h && cast_local(S, bv, ti, r, b, pre)) {
@@ -309,18 +356,14 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     for (;;) {
         const int c0 = 2 * k;
         bool h0, h1;
-        float t1 = -INFINITY;
+        float t0, t1;
+        pair_hit(bv.pair, k, r, ri, active, h0, h1, t0, t1);  // children 2k, 2k+1
         if (prune) {
-            float t0;
-            h0 = active && node_hit_t(bv.a[c0], bv.b[c0], r, ri, t0);
-            h1 = active && node_hit_t(bv.a[c0 + 1], bv.b[c0 + 1], r, ri, t1);
             const float ct = cut();
             h0 = h0 && !(t0 > ct);
             h1 = h1 && !(t1 > ct);
-        } else {
-            h0 = active && node_hit(bv.a[c0], bv.b[c0], r, ri);
-            h1 = active && node_hit(bv.a[c0 + 1], bv.b[c0 + 1], r, ri);
         }
+        if (STATS) wc.wpair++;
         if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
 #pragma nounroll
             for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : (h1 && !(prune && t1 > cut())), c0 + c - n);
@@ -591,6 +634,27 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     return acc;
 }
 
+// LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
+// (16-B aligned); lds_bytes() on the host must match.
+template <bool LDS>
+__device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
+    BvhRefs bv;
+    if (LDS) {
+        const int n3 = 3 * S.n_leaf;
+        float4* np = reinterpret_cast<float4*>(smem);
+        int* lf = reinterpret_cast<int*>(smem + 16 * (size_t)n3);
+        float4* in = reinterpret_cast<float4*>(smem + ((16 * (size_t)n3 + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15));
+        for (int i = threadIdx.x; i < n3; i += blockDim.x) np[i] = S.node_pair[i];
+        for (int i = threadIdx.x; i < S.n_leaf; i += blockDim.x) lf[i] = S.leaf_inst[i];
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        __syncthreads();
+        bv.pair = np; bv.leaf = lf; bv.inst = in;
+    } else {
+        bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    }
+    return bv;
+}
+
 __device__ __forceinline__ V4 shfl4(V4 v, int src) {
     return v4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
 }
@@ -608,21 +672,7 @@ constexpr int M_MULTI = 1, M_STATS = 2;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    BvhRefs bv;
-    if (LDS) {
-        const int n2 = 2 * S.n_leaf;
-        float4* a = reinterpret_cast<float4*>(smem);
-        float2* b = reinterpret_cast<float2*>(smem + 16 * (size_t)n2);
-        int* lf = reinterpret_cast<int*>(smem + 24 * (size_t)n2);
-        float4* in = reinterpret_cast<float4*>(smem + (((24 * (size_t)n2 + 4 * (size_t)S.n_leaf) + 15) & ~(size_t)15));
-        for (int i = threadIdx.x; i < n2; i += blockDim.x) { a[i] = S.node_a[i]; b[i] = S.node_b[i]; }
-        for (int i = threadIdx.x; i < S.n_leaf; i += blockDim.x) lf[i] = S.leaf_inst[i];
-        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
-        __syncthreads();
-        bv.a = a; bv.b = b; bv.leaf = lf; bv.inst = in;
-    } else {
-        bv.a = S.node_a; bv.b = S.node_b; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
-    }
+    const BvhRefs bv = stage_bvh<LDS>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
@@ -691,6 +741,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
         if (wc.leaves) atomicAdd(&P.stats[2], wc.leaves);
         if (wc.tris) atomicAdd(&P.stats[3], wc.tris);
+        atomicAdd(&P.stats[4], wc.wq); atomicAdd(&P.stats[5], wc.wpair);
+        atomicAdd(&P.stats[6], wc.wleaf); atomicAdd(&P.stats[7], wc.wtri);
     }
 }
 
@@ -700,21 +752,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
 template <bool LDS, bool NOLEAF, int WORK>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams P, SceneView S, float4* out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    BvhRefs bv;
-    if (LDS) {
-        const int n2 = 2 * S.n_leaf;
-        float4* a = reinterpret_cast<float4*>(smem);
-        float2* b = reinterpret_cast<float2*>(smem + 16 * (size_t)n2);
-        int* lf = reinterpret_cast<int*>(smem + 24 * (size_t)n2);
-        float4* in = reinterpret_cast<float4*>(smem + (((24 * (size_t)n2 + 4 * (size_t)S.n_leaf) + 15) & ~(size_t)15));
-        for (int i = threadIdx.x; i < n2; i += blockDim.x) { a[i] = S.node_a[i]; b[i] = S.node_b[i]; }
-        for (int i = threadIdx.x; i < S.n_leaf; i += blockDim.x) lf[i] = S.leaf_inst[i];
-        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
-        __syncthreads();
-        bv.a = a; bv.b = b; bv.leaf = lf; bv.inst = in;
-    } else {
-        bv.a = S.node_a; bv.b = S.node_b; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
-    }
+    const BvhRefs bv = stage_bvh<LDS>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L;
@@ -757,8 +795,7 @@ struct BvhArgs {
     int n;                   // padded leaf count (power of two)
     Box* boxes;              // scratch: n instance boxes
     Box* tree;               // scratch: 2n-1 boxes, reference storage order
-    float4* node_a;          // out: [2n] heap order (index 0 unused): (mnx, mny, mnz, mxx)
-    float2* node_b;          // out: [2n] (mxy, mxz); degenerate boxes: min=+inf, max=-inf
+    float* node_pair;        // out: [12n] child-pair layout (BvhRefs); degenerate boxes: min=+inf, max=-inf
     int* leaf_inst;          // out: [n] instance of leaf node n+i
 };
 
@@ -815,17 +852,14 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         lvl += size; out += size / 2; size >>= 1;
     }
     // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
-    for (int k = tid + 1; k < 2 * n; k += nt) {
-        const int s = 2 * n - 1 - k;
-        const Box b = A.tree[s];
-        if (b.nd) {
-            A.node_a[k] = make_float4(b.mn.x, b.mn.y, b.mn.z, b.mx.x);
-            A.node_b[k] = make_float2(b.mx.y, b.mx.z);
-        } else {
-            A.node_a[k] = make_float4(INFINITY, INFINITY, INFINITY, -INFINITY);
-            A.node_b[k] = make_float2(-INFINITY, -INFINITY);
-        }
-        if (k >= n) A.leaf_inst[k - n] = idx[s];
+    for (int k = tid; k < 2 * n; k += nt) {
+        Box b;
+        b.nd = 0;
+        if (k > 0) b = A.tree[2 * n - 1 - k];
+        if (!b.nd) { b.mn = v3(INFINITY, INFINITY, INFINITY); b.mx = v3(-INFINITY, -INFINITY, -INFINITY); }
+        float* q = A.node_pair + 12 * (k >> 1) + (k & 1);
+        q[0] = b.mn.x; q[2] = b.mn.y; q[4] = b.mn.z; q[6] = b.mx.x; q[8] = b.mx.y; q[10] = b.mx.z;
+        if (k >= n) A.leaf_inst[k - n] = idx[2 * n - 1 - k];
     }
 }
 
@@ -895,6 +929,26 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
             oi[i] = bx[6] != 0 && box_hit_f(L3(bx), L3(bx + 3), r, ray_inv(r));
             break;
         }
+        case 15: {   // packed child-pair box test (pair_hit): two boxes (mn, mx, nd) x 2 vs one ray
+            const float* bx = a + 14 * i;
+            float q[12];
+            for (int c = 0; c < 2; c++) {
+                const float* x = bx + 7 * c;
+                const bool nd = x[6] != 0;
+                for (int j = 0; j < 3; j++) {
+                    q[2 * j + c] = nd ? x[j] : INFINITY;
+                    q[6 + 2 * j + c] = nd ? x[3 + j] : -INFINITY;
+                }
+            }
+            const float4 np[3] = {make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]),
+                                  make_float4(q[8], q[9], q[10], q[11])};
+            Ray r = make_ray(L3(b + 6 * i), L3(b + 6 * i + 3));
+            bool h0, h1;
+            float t0, t1;
+            pair_hit(np, 0, r, ray_inv(r), true, h0, h1, t0, t1);
+            oi[2 * i] = h0; oi[2 * i + 1] = h1;
+            break;
+        }
         default: break;
     }
 }
@@ -913,7 +967,7 @@ struct rt_scene {
     // device buffers
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
     DLight* d_lights = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
-    float4* d_node_a = nullptr; float2* d_node_b = nullptr; int* d_leaf = nullptr; float4* d_inst4 = nullptr;
+    float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_inst4 = nullptr;
     int* d_work = nullptr; int n_cu = 0;
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
@@ -975,15 +1029,14 @@ int upload(rt_scene* s) {
     if (s->n_leaf > BVH_MAX_LEAVES) return fail(RT_ERR_LIMIT, "more than 8192 padded instances: single-workgroup BVH build limit");
     s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
-    HIPCHK(hipMalloc((void**)&s->d_node_a, 2 * nl * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&s->d_node_b, 2 * nl * sizeof(float2)));
+    HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_work, 16 * NQ * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
-    HIPCHK(hipMalloc((void**)&s->d_stats, 4 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&s->d_stats, 8 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
@@ -1002,6 +1055,11 @@ int upload_inst4(rt_scene* s) {
     }
     if (!v.empty()) HIPCHK(hipMemcpy(s->d_inst4, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice));
     return RT_OK;
+}
+
+// stage_bvh's LDS image size
+size_t lds_bytes(const SceneView& S) {
+    return ((48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + 16 * (size_t)S.n_inst;
 }
 
 int ensure_spp(rt_scene* s, int spp) {
@@ -1023,7 +1081,7 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.meshes = s->d_meshes; A.n_meshes = (int)s->h.d_meshes.size();
     A.tris = s->d_tris; A.n = s->n_leaf;
     A.boxes = s->d_boxes; A.tree = s->d_tree;
-    A.node_a = s->d_node_a; A.node_b = s->d_node_b; A.leaf_inst = s->d_leaf;
+    A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
@@ -1036,7 +1094,7 @@ int build_bvh(rt_scene* s, hipStream_t st) {
 SceneView view_of(const rt_scene* s, bool use_bvh) {
     SceneView v;
     v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
-    v.node_a = s->d_node_a; v.node_b = s->d_node_b; v.leaf_inst = s->d_leaf; v.inst4 = s->d_inst4;
+    v.node_pair = s->d_node_pair; v.leaf_inst = s->d_leaf; v.inst4 = s->d_inst4;
     v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
     v.ident_all = 1;
@@ -1087,9 +1145,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
-    // LDS image: node_a[2n] | node_b[2n] | leaf_inst[n] | (16-B aligned) inst4[n_inst]
-    size_t lds = (24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15;
-    lds += 16 * (size_t)S.n_inst;
+    const size_t lds = lds_bytes(S);
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
     const void* fn;
@@ -1135,7 +1191,7 @@ void invalidate(rt_scene* s) { s->bvh_valid = false; }
 rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
-    dfree(d_node_a); dfree(d_node_b); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
+    dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
@@ -1395,7 +1451,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         s->tev_used += 3;
         HIPCHK(hipEventRecord(te[0], st));
     }
-    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
+    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st)) != RT_OK) return r;
     }
@@ -1516,7 +1572,7 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
 int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_t* counters) {
     CHECK_FINISHED(s);
     int r;
-    if (which == 4) {
+    if (which == 4 || which == 5) {                           // full frame, counted kernel; 4: occlusion exit on
         if ((r = upload(s)) != RT_OK) return r;
         HIPCHK(hipSetDevice(s->device));
         if ((r = ensure_spp(s, spp)) != RT_OK) return r;
@@ -1524,17 +1580,17 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
-            HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), s->stream));
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), s->stream));
             HIPCHK(hipEventRecord(s->ev[0], s->stream));
-            if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, 1)) != RT_OK) return r;
+            if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0)) != RT_OK) return r;
             HIPCHK(hipEventRecord(s->ev[1], s->stream));
             HIPCHK(hipEventSynchronize(s->ev[1]));
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
-        unsigned long long v[4];
+        unsigned long long v[8];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-        if (counters) for (int i = 0; i < 4; i++) counters[i] = v[i];
+        if (counters) for (int i = 0; i < 8; i++) counters[i] = v[i];
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
@@ -1552,7 +1608,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     P.gw = gw; P.gh = P.px_per_wave / gw; P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     SceneView S = view_of(s, true);
-    size_t lds = ((24 * 2 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + 16 * (size_t)S.n_inst;
+    size_t lds = lds_bytes(S);
     const void* fn = which == 1 ? (const void*)primary_only_kernel<true, true, 0>
                    : which == 2 ? (const void*)primary_only_kernel<true, true, 1>
                    : which == 3 ? (const void*)primary_only_kernel<true, false, 1>
@@ -1566,7 +1622,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     float total = 0;
     for (int i = 0; i < reps; i++) {
         HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), s->stream));
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 4 * sizeof(unsigned long long), s->stream));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), s->stream));
         HIPCHK(hipEventRecord(s->ev[0], s->stream));
         void* args[] = {&P, &S, &out};
         HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, s->stream));
@@ -1575,9 +1631,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
-    unsigned long long v[4];
+    unsigned long long v[8];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 4; i++) counters[i] = v[i];
+    if (counters) for (int i = 0; i < 8; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;
@@ -1586,12 +1642,13 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
 int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2, float* of, int32_t* oi,
                   uint64_t* ou) {
     static const char* ops[] = {"normalize3", "cross", "reflect", "refract", "quat_rotate", "quat_inverse", "quat_mul",
-                                "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow", "tri_hit_f", "box_hit_f"};
+                                "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow", "tri_hit_f", "box_hit_f",
+                                "box_pair"};
     // per-op sizes (floats): in0, in1, in2, out_f, out_i, out_u per element
     static const int sz[][6] = {{3, 0, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 2, 3, 1, 0},
                                 {4, 3, 0, 3, 0, 0}, {4, 0, 0, 4, 0, 0}, {4, 4, 0, 4, 0, 0}, {9, 6, 0, 3, 1, 0},
                                 {6, 0, 0, 6, 0, 0}, {3, 0, 0, 0, 0, 1}, {4, 0, 0, 9, 0, 0}, {7, 6, 0, 0, 1, 0},
-                                {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}};
+                                {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}, {14, 6, 0, 0, 2, 0}};
     if (!op || n <= 0) return fail(RT_ERR_ARG, "bad arguments");
     int k = -1;
     for (int i = 0; i < (int)(sizeof ops / sizeof *ops); i++) if (!strcmp(op, ops[i])) k = i;
@@ -1609,13 +1666,13 @@ int rt_kat_device(const char* op, int n, const float* in0, const float* in1, con
             HIPCHK(hipMemcpy(din[i], hin[i], (size_t)n * sz[k][i] * 4, hipMemcpyHostToDevice));
         }
     if (sz[k][3]) HIPCHK(hipMalloc((void**)&dof, (size_t)n * sz[k][3] * 4));
-    if (sz[k][4]) HIPCHK(hipMalloc((void**)&doi, (size_t)n * 4));
+    if (sz[k][4]) HIPCHK(hipMalloc((void**)&doi, (size_t)n * sz[k][4] * 4));
     if (sz[k][5]) HIPCHK(hipMalloc((void**)&dou, (size_t)n * 8));
     hipLaunchKernelGGL(kat_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, k, n, din[0], din[1], din[2], dof, doi, dou);
     HIPCHK(hipGetLastError());
     HIPCHK(hipDeviceSynchronize());
     if (sz[k][3] && of) HIPCHK(hipMemcpy(of, dof, (size_t)n * sz[k][3] * 4, hipMemcpyDeviceToHost));
-    if (sz[k][4] && oi) HIPCHK(hipMemcpy(oi, doi, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (sz[k][4] && oi) HIPCHK(hipMemcpy(oi, doi, (size_t)n * sz[k][4] * 4, hipMemcpyDeviceToHost));
     if (sz[k][5] && ou) HIPCHK(hipMemcpy(ou, dou, (size_t)n * 8, hipMemcpyDeviceToHost));
     for (auto p : din) if (p) (void)hipFree(p);
     if (dof) (void)hipFree(dof);

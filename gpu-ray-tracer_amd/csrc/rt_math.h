@@ -104,9 +104,12 @@ RT_HD V3 qrot(Q q, V3 v) { return qrot_pre(qnormalized(q), qinverse(q), v); }
 // zero comes back as +0; `x + 0.0f` performs exactly that canonicalisation
 // and is not folded without fast-math.  Then |v| * normalize(v') follows.
 RT_HD V3 qrot_identity(V3 v) {
+    // = length * normalized(c).  len(c) == len(v) bit for bit: c differs from v only by
+    // -0 -> +0, whose square is the same +0, so normalized(c)'s length is `length`.
     float length = len(v);
     V3 c = v3(v.x + 0.0f, v.y + 0.0f, v.z + 0.0f);
-    return length * normalized(c);
+    V3 nc = length > THRESH ? (1 / length) * c : v3(0.0f, 0.0f, 0.0f);
+    return length * nc;
 }
 
 // ---- entity pose (entity.cu:5-37) with precomputed quaternion factors ----
@@ -231,13 +234,19 @@ RT_HD bool tri_hit(V3 a, V3 b, V3 c, V3 pn, float area, const Ray& r, float& tim
 //  * v_sqrt_f32 / v_rcp_f32 are within 1 ulp; a barycentric term b' =
 //    fl(sqrt'(s) * fl(1/area)) is within 6u of fl(fl(sqrt(s)) / area); the sum
 //    test uses a 32u margin.  The accepted (t, u, v) are always recomputed exactly.
-struct RayInv { float ix, iy, iz; int exact; };
+// b* = +inf for a zero direction component (the reference skips that slab): the packed
+// pair test forms q0 = fma(mn - o, inv, -b), q1 = fma(mx - o, inv, +b), i.e. (-inf, +inf)
+// = no constraint for a skipped axis and exactly fl((mn - o) * inv) otherwise.
+struct RayInv { float ix, iy, iz, bx, by, bz; int exact; };
 RT_HD RayInv ray_inv(const Ray& r) {
     RayInv v;
     v.ix = r.d.x != 0 ? 1.0f / r.d.x : 0.0f;
     v.iy = r.d.y != 0 ? 1.0f / r.d.y : 0.0f;
     v.iz = r.d.z != 0 ? 1.0f / r.d.z : 0.0f;
-    v.exact = !(isfinite(v.ix) && isfinite(v.iy) && isfinite(v.iz));
+    v.bx = r.d.x != 0 ? 0.0f : INFINITY;
+    v.by = r.d.y != 0 ? 0.0f : INFINITY;
+    v.bz = r.d.z != 0 ? 0.0f : INFINITY;
+    v.exact = !(isfinite(v.ix) && isfinite(v.iy) && isfinite(v.iz));   // subnormal components
     return v;
 }
 constexpr float FILT_BOX = 0x1p-20f;       // 16 u

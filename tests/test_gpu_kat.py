@@ -142,3 +142,20 @@ def test_filtered_triangle_adversarial(gpu, oracle):
     assert np.array_equal(hit.astype(bool), exp)
     assert np.array_equal(_bits(out[exp]), _bits(tuv[exp]))
     assert 0.1 < exp.mean() < 0.9
+
+
+def test_packed_pair_box_test_equals_exact(gpu, oracle):
+    """pair_hit (both children of a BVH pair, packed slab arithmetic, filtered with a
+    self-relative bound) == the reference slab test for each box, on face/edge/corner
+    targets, degenerate slots and rays with zero direction components."""
+    rng = np.random.default_rng(4242)
+    n = 200000
+    box, ray = _adversarial_boxes(rng, n)
+    box[rng.random(n) < 0.05, 6] = 0.0                        # degenerate (padding) boxes
+    other = np.roll(box, 1, axis=0)
+    ref0, _ = oracle.kat("box_hit", box, ray)
+    ref1, _ = oracle.kat("box_hit", other, ray)
+    out = gpu.kat_device("box_pair", np.concatenate([box, other], 1), ray)
+    assert np.array_equal(out[:, 0], ref0)
+    assert np.array_equal(out[:, 1], ref1)
+    assert 0.2 < ref0.mean() < 0.9
