@@ -79,6 +79,11 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     float prune_abs;          // distance-pruning slack M0 (< 0: pruning off), see closest_hit
 };
 
+// Parts of a DTri (rt_scene.h): the plane filter's 32-B head and the rest of the test.
+struct TriHot { V3 pn, a; float b_x, b_y; };
+struct TriRest { V3 b, c; float area, inv_area; };
+static_assert(sizeof(TriHot) == 32 && offsetof(DTri, b) == 24 && offsetof(DTri, inv_area) == 52, "DTri layout");
+
 // Wave-uniform read-only records in global memory are read through the
 // constant address space so that uniform indices compile to scalar (SMEM) loads.
 template <class T> __device__ __forceinline__ T ldc(const T* p, int i) {
@@ -93,6 +98,11 @@ template <class T> __device__ __forceinline__ T ldc(const T* p, int i) {
 #pragma unroll
     for (int w = 0; w < (int)(sizeof(T) / 4); w++) d[w] = s[w];
     return r;
+}
+
+__device__ __forceinline__ TriHot ld_hot(const DTri* T, int t) { return ldc(reinterpret_cast<const TriHot*>(T + t), 0); }
+__device__ __forceinline__ TriRest ld_rest(const DTri* T, int t) {
+    return ldc(reinterpret_cast<const TriRest*>(reinterpret_cast<const char*>(T + t) + 24), 0);
 }
 
 // Triangle test of Triangle::hit (geometry.h:273-290) fused with TriInner::tri_hit's
@@ -242,16 +252,25 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
     }
     int best = -1;
     float bu = 0.0f, bv_ = 0.0f, t_best = b.time;
+#if RT_FILTERED
+    // The plane filter needs only the 32-B head (pn, a) of each record (one batch of
+    // scalar loads); the rest is read only for triangles that pass it.
+    for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
+        const TriHot h = ld_hot(S.tris, t);
+        float denom, num, time, u, v;
+        if (!tri_plane_f(h.a, h.pn, mr, t_best, denom, num)) continue;
+        const TriRest q = ld_rest(S.tris, t);
+        if (tri_inside_f(h.a, q.b, q.c, q.area, q.inv_area, mr, t_best, denom, num, time, u, v)) {
+            t_best = time; best = t; bu = u; bv_ = v;
+        }
+    }
+#else
     for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
         const DTri T = ldc(S.tris, t);
         float time, u, v;
-#if RT_FILTERED
-        const bool acc = tri_accept_f(T.a, T.b, T.c, T.pn, T.area, T.inv_area, mr, t_best, time, u, v);
-#else
-        const bool acc = tri_accept(T, mr, t_best, time, u, v);
-#endif
-        if (acc) { t_best = time; best = t; bu = u; bv_ = v; }
+        if (tri_accept(T, mr, t_best, time, u, v)) { t_best = time; best = t; bu = u; bv_ = v; }
     }
+#endif
     if (best < 0) return false;
     b.time = (t_best * scale) * dir_len;                      // fix_isect, then cast_local
     b.inst = ti; b.tri = best; b.u = bu; b.v = bv_;

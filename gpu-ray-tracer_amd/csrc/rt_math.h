@@ -297,14 +297,18 @@ inline float fast_rcp(float x) { return 1.0f / x; }
 
 // tri_hit (above) + TriInner::tri_hit's acceptance (trimesh.cu:56), filtered.
 // inv_area = fl(1 / area) (host-precomputed; only used by the filter).
-RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, const Ray& r, float best,
-                        float& time, float& u, float& v) {
-    float denom = dot(r.d, pn);
+// Split in two so the trace kernel can start the next triangle's loads between them:
+// tri_plane_f needs only (pn, a) and rejects most triangles; tri_inside_f finishes.
+RT_HD bool tri_plane_f(V3 a, V3 pn, const Ray& r, float best, float& denom, float& num) {
+    denom = dot(r.d, pn);
     if (fabsf(denom) < THRESH) return false;
-    float num = dot(a - r.o, pn);
+    num = dot(a - r.o, pn);
     float ta = num * fast_rcp(denom);                    // ~1 ulp of the exact fl(fl(1/denom) * num)
     float et = fabsf(ta) * FILT_TRI + FILT_ABS;
-    if (ta + et < THRESH || ta - et >= best) return false;  // certainly rejected by t >= 1e-5 && t < best
+    return !(ta + et < THRESH || ta - et >= best);       // false: certainly rejected by t >= 1e-5 && t < best
+}
+RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray& r, float best, float denom,
+                        float num, float& time, float& u, float& v) {
     float t = (1.0f / denom) * num;                       // exact (geometry.h:259)
     if (!(t >= THRESH && t < best)) return false;
     V3 p = at(r, t);
@@ -318,6 +322,12 @@ RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, con
     float b0 = sqrtf(s0) / area;
     if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
     return false;
+}
+RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, const Ray& r, float best,
+                        float& time, float& u, float& v) {
+    float denom, num;
+    return tri_plane_f(a, pn, r, best, denom, num) &&
+           tri_inside_f(a, b, c, area, inv_area, r, best, denom, num, time, u, v);
 }
 
 // ---- quaternion <-> basis (geometry.h:36-41, 183-198) ----

@@ -34,8 +34,8 @@ struct CameraDesc {
 };
 
 // ---- device-ready records (all plain-old-data, 16-byte aligned) ----
-struct alignas(16) DTri {              // 96 B: hot part first (14 floats read per test)
-    rtm::V3 a, b, c, pn;               // vertices (mesh-local), normalized plane normal
+struct alignas(16) DTri {              // 96 B: the plane filter's (pn, a) first (one 32-B scalar load)
+    rtm::V3 pn, a, b, c;               // normalized plane normal, vertices (mesh-local)
     float area;                        // |cross(b-a, c-a)|
     float inv_area;                    // fl(1/area): only used by the filtered test's estimate
     rtm::V3 n0, n1, n2;                // vertex normals (generate_normals)
