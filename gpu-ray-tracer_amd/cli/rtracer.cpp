@@ -1,0 +1,123 @@
+// rtracer — headless front end with the reference's command line (src/main.cc:31-79).
+//
+//   rtracer -c world8.json [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K]
+//           [--width W --height H] [--out frame.ppm] [--debug X,Y]
+//
+// -c config (worldN.json), -b benchmark (one timed frame, "Time: X ms" as main.cc:210-216),
+// -r unoptimize (brute force, no BVH), -d kernel dimension (accepted; the HIP path
+// tiles itself), -s serial CPU path: not part of this build (the CPU restatement lives
+// in oracle/ as test infrastructure), so it is rejected.  Without -b the reference
+// opens an SDL window and renders continuously; headless, this renders --frames frames
+// (default 1) through rtracer::gpu::update_scene and prints the frame rate.  --spp > 1
+// uses the build's multi-sample extension (rt_render).  --debug X,Y runs debug_cast.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rtracer_amd.hpp"
+
+static void usage() {
+    std::fprintf(stderr,
+                 "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
+                 "               [--out FILE.ppm] [--debug X,Y]\n");
+}
+
+static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return false;
+    std::fprintf(f, "P6\n%d %d\n255\n", w, h);
+    std::vector<unsigned char> row(3 * (size_t)w);
+    for (int y = 0; y < h; y++) {
+        for (int x = 0; x < w; x++) {
+            const uint32_t v = px[(size_t)y * w + x];
+            row[3 * x] = (unsigned char)(v >> 24); row[3 * x + 1] = (unsigned char)(v >> 16);
+            row[3 * x + 2] = (unsigned char)(v >> 8);
+        }
+        std::fwrite(row.data(), 1, row.size(), f);
+    }
+    return std::fclose(f) == 0;
+}
+
+int main(int argc, char** argv) {
+    std::string config, out;
+    bool bench = false, unopt = false, serial = false;
+    int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto val = [&](const char* name) -> const char* {
+            if (i + 1 >= argc) { std::fprintf(stderr, "%s needs a value\n", name); usage(); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "-c" || a == "--config") config = val("-c");
+        else if (a == "-b" || a == "--bench") bench = true;
+        else if (a == "-r" || a == "--unoptimize") unopt = true;
+        else if (a == "-s" || a == "--serial") serial = true;
+        else if (a == "-d" || a == "--dim") dim = std::atoi(val("-d"));
+        else if (a == "--frames") frames = std::atoi(val("--frames"));
+        else if (a == "--spp") spp = std::atoi(val("--spp"));
+        else if (a == "--width") width = std::atoi(val("--width"));
+        else if (a == "--height") height = std::atoi(val("--height"));
+        else if (a == "--out") out = val("--out");
+        else if (a == "--debug") {
+            if (std::sscanf(val("--debug"), "%d,%d", &dbg_x, &dbg_y) != 2) { usage(); return 2; }
+        } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
+    }
+    if (config.empty()) { usage(); return 2; }
+    if (serial) {
+        std::fprintf(stderr, "-s (serial CPU path) is not part of this build: the reference CPU path is "
+                             "restated in oracle/ for testing only\n");
+        return 2;
+    }
+    if (frames < 1 || spp < 1) { usage(); return 2; }
+
+    // procedural::gpu::generate with optional canvas override; a bad config is reported
+    // and exits (the reference asserts)
+    rt_scene* handle = nullptr;
+    if (rt_scene_load_json(config.c_str(), width, height, &handle) != RT_OK) {
+        std::fprintf(stderr, "cannot load %s: %s\n", config.c_str(), rt_last_error());
+        return 1;
+    }
+    renv::gpu::Scene* scene = new renv::gpu::Scene(handle);
+    renv::Environment& env = scene->get_environment();
+    std::printf("Loaded scene\n");
+    const int W = env.get_canvas().get_width(), H = env.get_canvas().get_height();
+
+    std::vector<uint32_t> host;
+    auto draw = [&]() {
+        if (spp == 1) {
+            rtracer::gpu::update_scene(scene, dim, !unopt);
+        } else {
+            host.resize((size_t)W * H);
+            rt_render_opts o;
+            rt_render_opts_default(&o);
+            o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim;
+            o.rgba = host.data(); o.host_outputs = 1;
+            rtamd_detail::check(rt_render(scene->handle(), &o, nullptr), "rt_render");
+        }
+    };
+    if (bench) {
+        auto from = std::chrono::high_resolution_clock::now();
+        draw();
+        auto to = std::chrono::high_resolution_clock::now();
+        std::printf("Time: %g ms\n", std::chrono::duration<double, std::milli>(to - from).count());
+    } else {
+        auto from = std::chrono::high_resolution_clock::now();
+        for (int f = 0; f < frames; f++) draw();
+        auto to = std::chrono::high_resolution_clock::now();
+        std::printf("FPS: %g\n", frames / std::chrono::duration<double>(to - from).count());
+    }
+    if (dbg_x >= 0) {
+        std::printf("shooting debug ray at %d, %d\n", dbg_x, dbg_y);
+        rtracer::gpu::debug_cast(scene, dbg_x, dbg_y);
+    }
+    if (!out.empty()) {
+        const uint32_t* px = spp == 1 ? env.get_canvas().get_buffer() : host.data();
+        if (!px || !write_ppm(out.c_str(), px, W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
+    }
+    renv::gpu::Scene::free(*scene);
+    delete scene;
+    return 0;
+}

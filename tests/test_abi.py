@@ -52,3 +52,16 @@ def test_oracle_not_linked_into_product(rt):
     """The product library must not depend on or embed the oracle."""
     blob = open(rt.LIB_PATH, "rb").read()
     assert b"orc_render" not in blob and b"liboracle" not in blob
+
+
+def test_cpp_shim_and_cli_compile_against_the_abi(tmp_path):
+    """include/rtracer_amd.hpp (the reference's rtracer/renv/procedural C++ API over the C
+    ABI) compiles and links with a reference-style caller and with the CLI; nothing is
+    run here (no GPU in this container)."""
+    import subprocess
+    inc = os.path.join(ROOT, "include")
+    libdir = os.path.join(ROOT, "gpu-ray-tracer_amd")
+    for src in (os.path.join(ROOT, "tests", "shim_world.cpp"), os.path.join(libdir, "cli", "rtracer.cpp")):
+        r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, src, "-o", str(tmp_path / "a.out"),
+                            "-L", libdir, "-lrt_amd"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr

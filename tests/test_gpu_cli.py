@@ -1,0 +1,95 @@
+"""The reference-facing front ends on the GPU: the headless CLI with the reference's
+flags (gpu-ray-tracer_amd/cli/rtracer.cpp, main.cc:31-79) and a program written
+against the C++ shim (include/rtracer_amd.hpp: SceneBuilder / update_scene /
+get_canvas) -- both must produce the oracle's frame."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, scene_path
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(ROOT, "gpu-ray-tracer_amd", "rtracer")
+
+
+def _run(args, timeout=120):
+    return subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+
+
+def _ppm_rgb(path):
+    data = open(path, "rb").read()
+    head = data.split(b"\n", 3)
+    w, h = map(int, head[1].split())
+    return np.frombuffer(head[3], np.uint8).reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("flags,bvh", [(["-b"], 1), (["-b", "-r"], 0), (["--frames", "3", "-d", "8"], 1)])
+def test_cli_frame_matches_oracle(oracle, tmp_path, flags, bvh):
+    out = str(tmp_path / "f.ppm")
+    r = _run([CLI, "-c", scene_path("world8"), "--width", "200", "--height", "120", "--out", out] + flags)
+    assert r.returncode == 0, r.stderr
+    assert "Loaded scene" in r.stdout
+    assert ("Time: " in r.stdout) if "-b" in flags else ("FPS: " in r.stdout)
+    o = oracle.render(oracle.load(scene_path("world8"), 200, 120), use_bvh=bvh, spp=1, nthreads=8, want=("rgba",))
+    rgba = o["rgba"]
+    exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
+    assert np.array_equal(_ppm_rgb(out), exp)
+
+
+def test_cli_multisample_and_debug(tmp_path):
+    out = str(tmp_path / "f.ppm")
+    r = _run([CLI, "-c", scene_path("world8_stress"), "--width", "160", "--height", "90", "--spp", "4", "-b",
+              "--out", out, "--debug", "80,45"])
+    assert r.returncode == 0, r.stderr
+    assert "shooting debug ray at 80, 45" in r.stdout and "shooting a ray" in r.stdout
+    assert _ppm_rgb(out).shape == (90, 160, 3)
+
+
+def test_cli_rejects_serial_and_bad_args():
+    r = _run([CLI, "-c", scene_path("world1"), "-s"])
+    assert r.returncode == 2 and "serial" in r.stderr
+    assert _run([CLI]).returncode == 2
+    r = _run([CLI, "-c", "/nonexistent.json", "-b"])
+    assert r.returncode == 1 and "cannot load" in r.stderr
+
+
+def _write_desc(path, rt):
+    """world1 as a SceneBuilder description (the same construction test_scene.py checks)."""
+    ref = rt.Scene.load_json(scene_path("world1"), 96, 72)
+    R = ref.arrays()
+    doc = json.load(open(scene_path("world1")))
+    inv = np.float32(1) / np.float32(255)
+    fov = np.float32(np.float32(45 * np.pi) / np.float32(180))
+    cam, env = R["camera"], R["env"]
+    g = lambda xs: " ".join("%.9g" % float(x) for x in xs)
+    lines = ["96 72 %.9g %.9g %d" % (fov, cam[8], ref.info()["depth"]), g(cam[:7]), g(env[:7]), str(len(R["materials"]))]
+    lines += [g(m) for m in R["materials"]]
+    lines.append(str(len(R["instances"])))
+    lines += ["%d %s" % (m, g(q[4:7])) for q, m in zip(R["instances"], R["inst_mesh"])]
+    dirs = doc["lights"]["directional"]
+    lines.append(str(len(dirs)))
+    lines += [g(list(l["dir"]) + list(inv * np.float32(l["col"]))) for l in dirs]
+    pts = [l for l in R["lights"] if l[3] == 0]
+    lines.append(str(len(pts)))
+    lines += [g(list(l[:3]) + list(l[4:8])) for l in pts]
+    open(path, "w").write("\n".join(lines) + "\n")
+
+
+def test_cpp_shim_scene_builder_frame(gpu, oracle, tmp_path):
+    exe = str(tmp_path / "shim_world")
+    inc = os.path.join(ROOT, "include")
+    libdir = os.path.join(ROOT, "gpu-ray-tracer_amd")
+    r = _run(["g++", "-O1", "-std=c++17", "-I", inc, os.path.join(ROOT, "tests", "shim_world.cpp"), "-o", exe,
+              "-L", libdir, "-lrt_amd", "-Wl,-rpath," + libdir])
+    assert r.returncode == 0, r.stderr
+    desc, out = str(tmp_path / "w.txt"), str(tmp_path / "c.bin")
+    _write_desc(desc, gpu)
+    r = _run([exe, desc, out])
+    assert r.returncode == 0, r.stdout + r.stderr
+    frame = np.fromfile(out, np.uint32).reshape(72, 96)
+    o = oracle.render(oracle.load(scene_path("world1"), 96, 72), spp=1, nthreads=8, want=("rgba",))
+    assert np.array_equal(frame, o["rgba"])
+    assert (frame != 0).any()
