@@ -196,7 +196,7 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 // Per-lane work counters (rays/nodes/leaves/triangle tests, the reference's units) plus
 // wave-level step counts for the profiling experiment (query iterations, child-pair
 // steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
-struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri; };
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 
@@ -361,11 +361,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             wc.wleaf++;
             wc.wtri += tc;
         }
+        const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
         else if (h && cast_local(S, bv, ti, r, b, pre)) {
             hit = true;
             if (b.time <= occl_t) active = false;             // occluded: this lane is done
         }
+        if (STATS) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - c0;
     };
     if (n == 1) { leaf(hr, 0); return hit; }
     // one copy of the leaf code for both children (keeps the kernel small)
@@ -505,7 +507,9 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         top--;
         if (top >= 0) { cur = stk[top].f; fl |= 4; }
     };
+    unsigned long long c_post = 0;
     for (;;) {
+        if (STATS && c_post) { wc.cyc_post += __builtin_amdgcn_s_memtime() - c_post; c_post = 0; }
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
             if (st == ST_LIGHT) {
@@ -584,8 +588,11 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
         float occl = -1.0f;
         if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
+        const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl,
                                                    st == ST_WAIT_SHADOW ? max_t : INFINITY);
+        unsigned long long c1 = 0;
+        if (STATS) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
@@ -706,18 +713,22 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int q0 = blockIdx.x % NQ;
     const int per_q = (P.n_groups + NQ - 1) / NQ;
     int qi = 0;
-    auto take = [&](int q) {
-        int t = 0;
-        if (lane == 0) t = atomicAdd(&P.work[16 * ((q0 + q) % NQ)], 1);
-        return __shfl(t, 0);
+    // Lane 0 holds the raw result of the pending ticket request.  It is requested after
+    // the group's own global loads (vmcnt retires in order, so an earlier atomic would
+    // hold them up) and read only when the next group starts.
+    int pend = 0;
+    auto request = [&](int q) {
+        if (lane == 0) pend = atomicAdd(&P.work[16 * ((q0 + q) % NQ)], 1);
     };
-    int ticket = take(0);
+    auto resolve = [&]() { return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
+    request(0);
+    int ticket = resolve();
+    const unsigned long long c_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-        while (qi < NQ && ticket >= per_q) { qi++; if (qi < NQ) ticket = take(qi); }
+        while (qi < NQ && ticket >= per_q) { qi++; if (qi < NQ) { request(qi); ticket = resolve(); } }
         if (qi >= NQ) break;
         const int g = ((q0 + qi) % NQ) + NQ * ticket;
-        ticket = take(qi);                                     // prefetch the next ticket
-        if (g >= P.n_groups) continue;
+        if (g >= P.n_groups) { request(qi); ticket = resolve(); continue; }
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
         const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
@@ -733,7 +744,10 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
                 float2 o = P.spp_off[k];
                 r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
             }
+            if (rd == 0) request(qi);                          // next ticket, in flight during the trace
+            const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
             V4 c = trace_sample<NS, STATS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc);
+            if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
                 V4 v = shfl4(c, base + s);
                 if (sub == 0 && rd * L + s < P.spp) {
@@ -754,6 +768,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
+        ticket = resolve();
     }
     if (STATS && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
@@ -762,6 +777,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         if (wc.tris) atomicAdd(&P.stats[3], wc.tris);
         atomicAdd(&P.stats[4], wc.wq); atomicAdd(&P.stats[5], wc.wpair);
         atomicAdd(&P.stats[6], wc.wleaf); atomicAdd(&P.stats[7], wc.wtri);
+        atomicAdd(&P.stats[8], wc.cyc_q); atomicAdd(&P.stats[9], wc.cyc_leaf);
+        atomicAdd(&P.stats[10], __builtin_amdgcn_s_memtime() - c_start);
+        atomicAdd(&P.stats[11], wc.cyc_sample); atomicAdd(&P.stats[12], wc.cyc_post);
     }
 }
 
@@ -1055,7 +1073,7 @@ int upload(rt_scene* s) {
     if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
-    HIPCHK(hipMalloc((void**)&s->d_stats, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&s->d_stats, 16 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
@@ -1470,7 +1488,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         s->tev_used += 3;
         HIPCHK(hipEventRecord(te[0], st));
     }
-    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
+    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st)) != RT_OK) return r;
     }
@@ -1599,7 +1617,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
-            HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), s->stream));
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), s->stream));
             HIPCHK(hipEventRecord(s->ev[0], s->stream));
             if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0)) != RT_OK) return r;
             HIPCHK(hipEventRecord(s->ev[1], s->stream));
@@ -1607,9 +1625,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
-        unsigned long long v[8];
+        unsigned long long v[13];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-        if (counters) for (int i = 0; i < 8; i++) counters[i] = v[i];
+        if (counters) for (int i = 0; i < 13; i++) counters[i] = v[i];
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
@@ -1641,7 +1659,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     float total = 0;
     for (int i = 0; i < reps; i++) {
         HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), s->stream));
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 8 * sizeof(unsigned long long), s->stream));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), s->stream));
         HIPCHK(hipEventRecord(s->ev[0], s->stream));
         void* args[] = {&P, &S, &out};
         HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, s->stream));
@@ -1650,9 +1668,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
-    unsigned long long v[8];
+    unsigned long long v[13];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 8; i++) counters[i] = v[i];
+    if (counters) for (int i = 0; i < 13; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;
