@@ -196,7 +196,7 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 // Per-lane work counters (rays/nodes/leaves/triangle tests, the reference's units) plus
 // wave-level step counts for the profiling experiment (query iterations, child-pair
 // steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
-struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post; };
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 
@@ -230,8 +230,12 @@ __device__ __forceinline__ DirPre dir_pre(V3 d) {
     return p;
 }
 
+// t_lo: lower bound of any acceptable local time (-inf if none): the leaf box's entry
+// distance minus the pruning slack M (closest_hit).  A triangle whose plane crossing is
+// certainly below it lies outside the box, so its inside test is skipped.
+template <bool STATS>
 __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b,
-                                           const DirPre& pre) {
+                                           const DirPre& pre, WaveCounters& wc, float t_lo) {
     int mesh_id;
     const Pose ip = inst_pose(S, bv, ti, mesh_id);
     mesh_id = uni(mesh_id);
@@ -258,7 +262,13 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
     for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
         const TriHot h = ld_hot(S.tris, t);
         float denom, num, time, u, v;
-        if (!tri_plane_f(h.a, h.pn, mr, t_best, denom, num)) continue;
+        const bool pass = tri_plane_f(h.a, h.pn, mr, t_best, t_lo, denom, num);
+        if (STATS) {
+            const unsigned long long pm = __ballot(pass);
+            wc.wbary += pm != 0;
+            wc.lbary += __popcll(pm);
+        }
+        if (!pass) continue;
         const TriRest q = ld_rest(S.tris, t);
         if (tri_inside_f(h.a, q.b, q.c, q.area, q.inv_area, mr, t_best, denom, num, time, u, v)) {
             t_best = time; best = t; bu = u; bv_ = v;
@@ -304,25 +314,36 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 // Light::attenuate returns 0 either way (light.cu:39-45).  Counters then count
 // the work done, so it is only used when statistics are not requested.
 //
-// Distance pruning (frames without statistics, S.prune_abs >= 0): a lane skips a
-// subtree/leaf whose box entry bound tlo exceeds cut = c + M, c = min(b.time, lim).
-// Exact: the subtree's leaves are processed later with b.time <= c, and none of
-// their triangles can be accepted.  An accepted local time t satisfies
-// t >= tmin_box - M: the hit point is within 1e-5 x (triangle size) of its triangle
-// (the barycentric-sum tolerance, geometry.h:281-286), the triangle is inside the
+// Box bound on acceptable times (S.prune_abs >= 0).  Claim: a triangle of a leaf can
+// only be accepted at a local time t >= tmin(box) - M(t).  The accepted point lies
+// within eps of its triangle (the barycentric-sum tolerance 1e-5 of geometry.h:
+// 281-286 allows ~1e-5 x triangle size in its plane), the triangle lies in the leaf
 // box when every pose is a pure translation and mesh offsets are zero (the host
-// checks), the pose chains round by O(u |coords|) and tlo <= tmin.  M = prune_abs
-// (1e-4 x mesh size + 2^-14 x scene radius) + 2^-14 c covers these with a wide
-// factor.  `lim` = max_t for shadow segments: hits beyond it never change
-// Light::attenuate (light.cu:35-58).
+// checks; the boxes ignore the mesh pose, raytracer.cu:54-89), and the local ray
+// differs from the world ray by O(u (|coords| + t)).  So the world ray is within
+// eps + delta of the box at time t, i.e. inside the box grown by that distance,
+// whose slab entry is >= tmin - (eps + delta) * max_a |1/d_a| (a zero component is
+// no constraint, a subnormal one gives an infinite bound).  The slack used is
+// M(t) = (prune_abs + 2^-14 |t|) * im + 2^-14 |t|, im = max_a |1/d_a|, prune_abs =
+// 4e-4 x max vertex coordinate + 2^-14 x scene radius: >= 20x the tolerance terms.
+// Uses (both exact):
+//  * distance pruning (frames without statistics): a lane skips a subtree whose box
+//    entry bound tlo exceeds c + M(c), c = min(b.time, lim).  Its leaves would be
+//    processed with b.time <= c and nothing in them can be accepted (a nested box is
+//    entered no earlier).  `lim` = max_t for shadow segments: hits beyond it never
+//    change Light::attenuate (light.cu:35-58).
+//  * triangle skip (cast_local's t_lo): a triangle whose plane crossing is certainly
+//    before tlo(leaf) - M cannot be accepted, so its inside test is not run.
 template <bool NOLEAF, bool STATS>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
     const bool prune = !STATS && S.prune_abs >= 0.0f;
+    float im = 0.0f;                                           // max_a |1/d_a| (set below)
+    auto slack = [&](float t) { return (S.prune_abs + 0x1p-14f * fabsf(t)) * im + 0x1p-14f * fabsf(t); };
     auto cut = [&]() {
         const float c = fminf(b.time, lim);
-        return c + (S.prune_abs + 0x1p-14f * c);
+        return c + slack(c);
     };
     bool active = active_in;
     const unsigned long long am = __ballot(active);
@@ -336,12 +357,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 wc.leaves += __popcll(am);
                 wc.tris += (unsigned long long)__popcll(am) * ldc(S.meshes, uni(__float_as_int(bv.inst[i].w) & 0x7fffffff)).tri_count;
             }
-            if (active && cast_local(S, bv, i, r, b, pre)) hit = true;
+            if (active && cast_local<STATS>(S, bv, i, r, b, pre, wc, -INFINITY)) hit = true;
         }
         return hit;
     }
     const int n = S.n_leaf;
     const RayInv ri = ray_inv(r);
+    im = ri.exact ? INFINITY : fmaxf(fabsf(ri.ix), fmaxf(fabsf(ri.iy), fabsf(ri.iz)));
     if (STATS) wc.nodes += __popcll(am);                       // root test
     bool hr, hdummy;
     float tdummy, troot;
@@ -350,7 +372,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     if (!br) return false;
     DirPre pre{};
     if (S.ident_all) pre = dir_pre(r.d);
-    auto leaf = [&](bool h, int li) {
+    // lower bound of acceptable local times in a leaf entered at >= tl (see distance pruning)
+#ifndef RT_BOXBOUND_STATS
+#define RT_BOXBOUND_STATS 0  // 1: profiling variant, counted kernels also skip inside tests
+#endif
+    const bool box_bound = (RT_BOXBOUND_STATS || !STATS) && S.prune_abs >= 0.0f;   // counted kernel: plain reference path
+    auto t_low = [&](float tl) { return box_bound ? tl - slack(tl) : -INFINITY; };
+    auto leaf = [&](bool h, int li, float tl) {
         const unsigned long long m = __ballot(h);
         if (!m) return;
         const int ti = uni(bv.leaf[li]);                       // leaf instance: wave-uniform
@@ -363,13 +391,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         }
         const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         if (NOLEAF) { if (h) { hit = true; b.inst = ti; } }
-        else if (h && cast_local(S, bv, ti, r, b, pre)) {
+        else if (h && cast_local<STATS>(S, bv, ti, r, b, pre, wc, t_low(tl))) {
             hit = true;
             if (b.time <= occl_t) active = false;             // occluded: this lane is done
         }
         if (STATS) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - c0;
     };
-    if (n == 1) { leaf(hr, 0); return hit; }
+    if (n == 1) { leaf(hr, 0, troot); return hit; }
     // one copy of the leaf code for both children (keeps the kernel small)
     if (STATS) wc.nodes += 2ull * __popcll(br);
     int k = 1;
@@ -387,7 +415,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         if (STATS) wc.wpair++;
         if (c0 >= n) {                                         // children are leaves: DFS order 2k, 2k+1
 #pragma nounroll
-            for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : (h1 && !(prune && t1 > cut())), c0 + c - n);
+            for (int c = 0; c < 2; c++) leaf(c == 0 ? h0 : (h1 && !(prune && t1 > cut())), c0 + c - n, c == 0 ? t0 : t1);
             if (!__ballot(active)) break;                      // every lane occluded
         } else {
             const unsigned long long b0 = __ballot(h0), b1 = __ballot(h1);
@@ -780,6 +808,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         atomicAdd(&P.stats[8], wc.cyc_q); atomicAdd(&P.stats[9], wc.cyc_leaf);
         atomicAdd(&P.stats[10], __builtin_amdgcn_s_memtime() - c_start);
         atomicAdd(&P.stats[11], wc.cyc_sample); atomicAdd(&P.stats[12], wc.cyc_post);
+        atomicAdd(&P.stats[13], wc.wbary); atomicAdd(&P.stats[14], wc.lbary);
     }
 }
 
@@ -1625,9 +1654,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
-        unsigned long long v[13];
+        unsigned long long v[15];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-        if (counters) for (int i = 0; i < 13; i++) counters[i] = v[i];
+        if (counters) for (int i = 0; i < 15; i++) counters[i] = v[i];
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
@@ -1668,9 +1697,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
-    unsigned long long v[13];
+    unsigned long long v[15];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 13; i++) counters[i] = v[i];
+    if (counters) for (int i = 0; i < 15; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;

@@ -299,13 +299,15 @@ inline float fast_rcp(float x) { return 1.0f / x; }
 // inv_area = fl(1 / area) (host-precomputed; only used by the filter).
 // Split in two so the trace kernel can start the next triangle's loads between them:
 // tri_plane_f needs only (pn, a) and rejects most triangles; tri_inside_f finishes.
-RT_HD bool tri_plane_f(V3 a, V3 pn, const Ray& r, float best, float& denom, float& num) {
+// `lo` (<= 1e-5 when unused): a proven lower bound of any acceptable t (the leaf box's
+// entry distance minus the pruning slack, see closest_hit in rt_kernels.hip).
+RT_HD bool tri_plane_f(V3 a, V3 pn, const Ray& r, float best, float lo, float& denom, float& num) {
     denom = dot(r.d, pn);
     if (fabsf(denom) < THRESH) return false;
     num = dot(a - r.o, pn);
     float ta = num * fast_rcp(denom);                    // ~1 ulp of the exact fl(fl(1/denom) * num)
     float et = fabsf(ta) * FILT_TRI + FILT_ABS;
-    return !(ta + et < THRESH || ta - et >= best);       // false: certainly rejected by t >= 1e-5 && t < best
+    return !(ta + et < fmaxf(THRESH, lo) || ta - et >= best);   // false: certainly rejected
 }
 RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray& r, float best, float denom,
                         float num, float& time, float& u, float& v) {
@@ -326,7 +328,7 @@ RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray&
 RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, const Ray& r, float best,
                         float& time, float& u, float& v) {
     float denom, num;
-    return tri_plane_f(a, pn, r, best, denom, num) &&
+    return tri_plane_f(a, pn, r, best, -INFINITY, denom, num) &&
            tri_inside_f(a, b, c, area, inv_area, r, best, denom, num, time, u, v);
 }
 

@@ -158,3 +158,21 @@ def test_fast_kernel_exact_close_camera(gpu, oracle):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+
+
+def test_fast_kernel_exact_grazing_rays(gpu):
+    """Distance pruning and the triangle skip near their worst case: level cameras placed
+    exactly on cube face planes and edges (faces at k +- 0.4995), so rays graze faces and
+    run along edges at shallow angles, where the slack's max|1/d| factor matters."""
+    import math
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    e = 0.4995
+    for pos, yaw in (([e, 3 + e, -8.0], 0.0), ([-1.0, 5 + e, -7.3], 0.0), ([e, 3 + e, -8.0], 1e-3),
+                     ([-4 - e, 1 + e, -6.0], 2e-4), ([0.25, 11 + e, -6.5], -5e-4)):
+        s.set_camera(pos, [0.0, math.sin(yaw / 2), 0.0, math.cos(yaw / 2)])
+        fast = s.render(spp=2, want=want, stats=False)
+        full = s.render(spp=2, want=want, stats=True)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, yaw, k)
+        assert (full["hit_inst"] >= 0).mean() > 0.05, pos

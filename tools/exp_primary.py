@@ -11,7 +11,7 @@ L.rt_experiment.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.
 scene = sys.argv[1] if len(sys.argv) > 1 else "world8_stress"
 for which, spp in [(int(w), 8) for w in (sys.argv[2].split(',') if len(sys.argv) > 2 else ['3', '2', '4'])]:
     s = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", scene + ".json"), 1920, 1080)
-    ms = ctypes.c_double(); c = (ctypes.c_uint64 * 13)()
+    ms = ctypes.c_double(); c = (ctypes.c_uint64 * 15)()
     rtamd._check(L.rt_experiment(s._h, which, spp, 6, ctypes.byref(ms), c))
     print(json.dumps({"scene": scene, "which": which, "lib": os.path.basename(rtamd.LIB_PATH), "spp": spp, "ms": ms.value, "rays": c[0], "nodes": c[1], "leaves": c[2],
                       "Mrays_s": c[0] / ms.value / 1e3,
@@ -19,4 +19,5 @@ for which, spp in [(int(w), 8) for w in (sys.argv[2].split(',') if len(sys.argv)
                       "lane_util_queries": c[0] / max(1, 64 * c[4]), "lane_util_pairs": c[1] / max(1, 128 * c[5] + 64 * c[4]),
                       "lane_util_leaves": c[2] / max(1, 64 * c[6]),
                       "frac_cycles_in_queries": c[8] / max(1, c[10]), "frac_cycles_in_leaves": c[9] / max(1, c[10]),
-                      "frac_cycles_in_samples": c[11] / max(1, c[10]), "frac_cycles_post_query": c[12] / max(1, c[10])}))
+                      "frac_cycles_in_samples": c[11] / max(1, c[10]), "frac_cycles_post_query": c[12] / max(1, c[10]),
+                      "wave_inside_tests": c[13], "lane_inside_tests": c[14]}))
