@@ -53,6 +53,7 @@ constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LD
 #endif
 constexpr int TRACE_BLOCK_P = RT_BLOCK;  // persistent block: 12 waves (3 per SIMD, 168-VGPR budget) sharing one LDS BVH copy
 constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
+constexpr int PARK_LDS_LIMIT = 158 * 1024;   // BVH image + parking area (160 KB per CU)
 constexpr int NQ = 8;                    // work queues (one per XCD dispatch slot), 64-B apart
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
@@ -507,9 +508,15 @@ __device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
 // pixel's sample 0 and records the primary hit ids there.
 enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_WAIT_SHADOW = 4 };
 
-template <int NS, bool STATS>
+// Parking (PARK): integrator state the traversal never reads is written to this lane's
+// LDS column before each query and read back after it, so the query runs with those
+// registers free (instead of the allocator spilling to scratch, whose working set is
+// larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
+// stop the compiler from forwarding the stored values and keeping them live.
+constexpr int PARK_FIELDS = 25;
+template <int NS, bool STATS, bool PARK>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
-                                           Ray r0, bool me, int out_p, WaveCounters& wc) {
+                                           Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     Frame cur;
     SavedFrame stk[NS > 0 ? NS : 1];
     int top = -1, st = ST_DONE;
@@ -616,9 +623,34 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
         float occl = -1.0f;
         if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
+        const float lim = st == ST_WAIT_SHADOW ? max_t : INFINITY;
+        if (PARK) {
+            float* pk = park;
+            int f = 0;
+            auto put = [&](float v) { pk[(f++) * TRACE_BLOCK_P] = v; };
+            put(cur.ray.o.x); put(cur.ray.o.y); put(cur.ray.o.z); put(cur.ray.d.x); put(cur.ray.d.y); put(cur.ray.d.z);
+            put(cur.atten.x); put(cur.atten.y); put(cur.atten.z); put(cur.atten.w);
+            put(acc.x); put(acc.y); put(acc.z); put(acc.w);
+            put(summed.x); put(summed.y); put(summed.z); put(summed.w);
+            put(rv.x); put(rv.y); put(rv.z); put(rv.w);
+            put(dtl.x); put(dtl.y); put(dtl.z);
+            asm volatile("" ::: "memory");
+        }
         const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl,
-                                                   st == ST_WAIT_SHADOW ? max_t : INFINITY);
+        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl, lim);
+        if (PARK) {
+            asm volatile("" ::: "memory");
+            const float* pk = park;
+            int f = 0;
+            auto get = [&]() { return pk[(f++) * TRACE_BLOCK_P]; };
+            cur.ray.o.x = get(); cur.ray.o.y = get(); cur.ray.o.z = get();
+            cur.ray.d.x = get(); cur.ray.d.y = get(); cur.ray.d.z = get();
+            cur.atten.x = get(); cur.atten.y = get(); cur.atten.z = get(); cur.atten.w = get();
+            acc.x = get(); acc.y = get(); acc.z = get(); acc.w = get();
+            summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
+            rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get();
+            dtl.x = get(); dtl.y = get(); dtl.z = get();
+        }
         unsigned long long c1 = 0;
         if (STATS) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
         if (!need) continue;
@@ -688,6 +720,11 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     return acc;
 }
 
+// stage_bvh's LDS image size (16-B multiple)
+__host__ __device__ inline size_t lds_bytes(const SceneView& S) {
+    return ((48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + ((16 * (size_t)S.n_inst + 15) & ~(size_t)15);
+}
+
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
 template <bool LDS>
@@ -722,7 +759,9 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // then stay live across rounds, which the common single-round kernel avoids).
 // MODE bit 1 (STATS): exact work counters.  The divergent state machine keeps 64-bit
 // counters in VGPRs, so frames without statistics use a kernel without them.
-constexpr int M_MULTI = 1, M_STATS = 2;
+// MODE bit 2 (PARK): park integrator state in LDS during queries (trace_sample); needs
+// PARK_FIELDS x 4 B x TRACE_BLOCK_P of LDS beside the BVH image.
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -730,7 +769,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
-    constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0;
+    constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
@@ -774,7 +814,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             }
             if (rd == 0) request(qi);                          // next ticket, in flight during the trace
             const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc);
+            V4 c = trace_sample<NS, STATS, PARK>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+                                                 park);
             if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
                 V4 v = shfl4(c, base + s);
@@ -1123,11 +1164,6 @@ int upload_inst4(rt_scene* s) {
     return RT_OK;
 }
 
-// stage_bvh's LDS image size
-size_t lds_bytes(const SceneView& S) {
-    return ((48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + 16 * (size_t)S.n_inst;
-}
-
 int ensure_spp(rt_scene* s, int spp) {
     if (spp <= s->spp_cap) return RT_OK;
     int cap = std::max(spp, 64);
@@ -1222,10 +1258,15 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, false, 2>, (const void*)trace_kernel<NG, false, 3>},
         {(const void*)trace_kernel<NG, true, 0>, (const void*)trace_kernel<NG, true, 1>,
          (const void*)trace_kernel<NG, true, 2>, (const void*)trace_kernel<NG, true, 3>}};
-    if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
+    const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
+    const bool park = mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
+    if (park) {
+        fn = ns <= 0 ? (const void*)trace_kernel<0, true, M_PARK> : ns <= 2 ? (const void*)trace_kernel<2, true, M_PARK>
+                     : (const void*)trace_kernel<NG, true, M_PARK>;
+    } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = use_lds ? lds : 0;
+    const size_t shm = park ? lds + park_bytes : use_lds ? lds : 0;
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
