@@ -291,8 +291,8 @@ RT_HD bool box_hit_ft(V3 mn, V3 mx, const Ray& r, const RayInv& ri, float& tlo) 
 __device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 #else
-inline float fast_sqrt(float x) { return sqrtf(x); }
-inline float fast_rcp(float x) { return 1.0f / x; }
+RT_HD float fast_sqrt(float x) { return sqrtf(x); }
+RT_HD float fast_rcp(float x) { return 1.0f / x; }
 #endif
 
 // tri_hit (above) + TriInner::tri_hit's acceptance (trimesh.cu:56), filtered.
