@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=8)
     p.add_argument("--brute", action="store_true", help="reference -r: no BVH")
+    p.add_argument("--textures", action="store_true",
+                   help="build-defined textured shading with the scene's atlas (e.g. --scene world16_tex, config 5)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-rows", type=int, default=1, help="CPU baseline renders rows y %% k == 0")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -97,6 +99,8 @@ def main():
     rtamd.set_device(local)
     scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")
     scene = rtamd.Scene.load_json(scene_path, args.width, args.height)
+    if args.textures:
+        scene.load_atlas()
     W, H = scene.width, scene.height
     my_rows = len(rtdist.rows_of(rank, world, H))
     fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist)
@@ -106,12 +110,14 @@ def main():
 
     def step(timing):
         scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
-                            compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, timing=timing)
+                            compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, timing=timing,
+                            textures=args.textures)
         fb.gather()
 
     # per-frame work counters (deterministic): one untimed counted render of this rank's rows
     st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
-                             compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, sync=True, stats=True)
+                             compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, sync=True, stats=True,
+                             textures=args.textures)
     for _ in range(args.warmup):
         step(False)
     scene.timing_collect()
@@ -169,7 +175,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32",
         "data": "procedural scene from the reference's %s.json (deterministic, no RNG at render time)" % args.scene,
-        "config": {"workload": "%s.json %dx%d %dspp %s" % (args.scene, W, H, args.spp, "brute" if args.brute else "BVH"),
+        "config": {"workload": "%s.json %dx%d %dspp %s%s" % (args.scene, W, H, args.spp, "brute" if args.brute else "BVH",
+                                                          " textured" if args.textures else ""),
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bvh": use_bvh,
                    "parallelism": "row-cyclic x%d + RCCL gather" % world if world > 1 else "single GPU"},
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),

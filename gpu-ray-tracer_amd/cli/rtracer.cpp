@@ -1,7 +1,7 @@
 // rtracer — headless front end with the reference's command line (src/main.cc:31-79).
 //
 //   rtracer -c world8.json [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K]
-//           [--width W --height H] [--out frame.ppm] [--debug X,Y]
+//           [--width W --height H] [--out frame.ppm] [--debug X,Y] [--textures [ATLAS.png]]
 //
 // -c config (worldN.json), -b benchmark (one timed frame, "Time: X ms" as main.cc:210-216),
 // -r unoptimize (brute force, no BVH), -d kernel dimension (accepted; the HIP path
@@ -10,6 +10,8 @@
 // opens an SDL window and renders continuously; headless, this renders --frames frames
 // (default 1) through rtracer::gpu::update_scene and prints the frame rate.  --spp > 1
 // uses the build's multi-sample extension (rt_render).  --debug X,Y runs debug_cast.
+// --textures turns on the build-defined textured shading mode with the scene's atlas
+// (or the given PNG).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -22,7 +24,7 @@
 static void usage() {
     std::fprintf(stderr,
                  "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
-                 "               [--out FILE.ppm] [--debug X,Y]\n");
+                 "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]]\n");
 }
 
 static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
@@ -43,7 +45,8 @@ static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
 
 int main(int argc, char** argv) {
     std::string config, out;
-    bool bench = false, unopt = false, serial = false;
+    bool bench = false, unopt = false, serial = false, textures = false;
+    std::string atlas;
     int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -61,6 +64,10 @@ int main(int argc, char** argv) {
         else if (a == "--width") width = std::atoi(val("--width"));
         else if (a == "--height") height = std::atoi(val("--height"));
         else if (a == "--out") out = val("--out");
+        else if (a == "--textures") {
+            textures = true;
+            if (i + 1 < argc && argv[i + 1][0] != '-') atlas = argv[++i];
+        }
         else if (a == "--debug") {
             if (std::sscanf(val("--debug"), "%d,%d", &dbg_x, &dbg_y) != 2) { usage(); return 2; }
         } else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 2; }
@@ -80,6 +87,10 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "cannot load %s: %s\n", config.c_str(), rt_last_error());
         return 1;
     }
+    if (textures && rt_scene_load_atlas(handle, atlas.empty() ? nullptr : atlas.c_str()) != RT_OK) {
+        std::fprintf(stderr, "cannot load the atlas: %s\n", rt_last_error());
+        return 1;
+    }
     renv::gpu::Scene* scene = new renv::gpu::Scene(handle);
     renv::Environment& env = scene->get_environment();
     std::printf("Loaded scene\n");
@@ -87,13 +98,13 @@ int main(int argc, char** argv) {
 
     std::vector<uint32_t> host;
     auto draw = [&]() {
-        if (spp == 1) {
+        if (spp == 1 && !textures) {
             rtracer::gpu::update_scene(scene, dim, !unopt);
         } else {
             host.resize((size_t)W * H);
             rt_render_opts o;
             rt_render_opts_default(&o);
-            o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim;
+            o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
             o.rgba = host.data(); o.host_outputs = 1;
             rtamd_detail::check(rt_render(scene->handle(), &o, nullptr), "rt_render");
         }
@@ -114,7 +125,7 @@ int main(int argc, char** argv) {
         rtracer::gpu::debug_cast(scene, dbg_x, dbg_y);
     }
     if (!out.empty()) {
-        const uint32_t* px = spp == 1 ? env.get_canvas().get_buffer() : host.data();
+        const uint32_t* px = (spp == 1 && !textures) ? env.get_canvas().get_buffer() : host.data();
         if (!px || !write_ppm(out.c_str(), px, W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
     }
     renv::gpu::Scene::free(*scene);

@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <fstream>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -439,9 +440,10 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
 // ---------------------------------------------------------------------------
 // Shading: phong.cu:14-53, light.cu:11-77, scene.cu:14-22
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ V4 phong(const DMat& m, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
+// kd: the material's Kd (the reference), or the atlas texel in the textured mode
+__device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
     float nd = max_std(dot(to_light, nrm), 0.0f);
-    V4 diffuse = nd * m.Kd;
+    V4 diffuse = nd * kd;
     V3 reflected = reflect(neg(to_light), nrm);
     float rd = dot(neg(reflected), ray_dir);
     V4 specular = pow_ref(max_std(rd, 0.0f), m.alpha) * m.Ks;
@@ -473,9 +475,28 @@ struct TraceParams {
     unsigned long long* stats;
     int* work;                // persistent-wave work counter (zeroed before each launch)
     int occl_exit;            // shadow-ray occlusion early exit (all-opaque scene, no statistics)
+    const float4* atlas;      // textured mode: atlas texels, byte / 255 (rt_scene_set_atlas)
+    int atlas_w, atlas_h;
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
 };
+
+// Textured mode (build-defined; phong.cu:18-23 leaves texture mapping a TODO): the
+// diffuse colour of a hit on a triangle with TextureCoords is the atlas texel at
+// (tx, ty) + u (ux, uy) + v (vx, vy), clamped to the atlas and truncated to a texel
+// index (point sampling, clamp addressing: the reference's texture setup); other hits
+// keep the material's Kd.  gfx950 has no image/sampler instructions (HIP marks tex2D
+// unavailable there), so the atlas is a plain float4 array in HBM.
+__device__ __forceinline__ V4 hit_kd(const TraceParams& P, const SceneView& S, const Best& b, int mat) {
+    const DTri& T = S.tris[b.tri];
+    if (!T.tex) return S.mats[mat].Kd;
+    const float x = (T.tx + b.u * T.ux) + b.v * T.vx;
+    const float y = (T.ty + b.u * T.uy) + b.v * T.vy;
+    const int ix = (int)fminf(fmaxf(x, 0.0f), (float)(P.atlas_w - 1));
+    const int iy = (int)fminf(fmaxf(y, 0.0f), (float)(P.atlas_h - 1));
+    const float4 c = P.atlas[(size_t)iy * P.atlas_w + ix];
+    return v4(c.x, c.y, c.z, c.w);
+}
 
 // Opaque to the optimiser: values derived from x (64-bit output addresses) are formed
 // here instead of being hoisted to the group start and spilled across the trace.
@@ -514,7 +535,7 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
 constexpr int PARK_FIELDS = 25;
-template <int NS, bool STATS, bool PARK>
+template <int NS, bool STATS, bool PARK, bool TEX>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     Frame cur;
@@ -527,6 +548,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     float is_time = INFINITY;                                   // the sample's shared Isect
     V3 is_norm = v3(0, 0, 0);
     int is_mat = 0;
+    V4 is_kd = v4(0, 0, 0, 0);                                  // textured mode: the hit's diffuse colour
     int li = 0;
     V4 summed = v4(0, 0, 0, 0), rv = v4(0, 0, 0, 0);
     V3 dtl = v3(0, 0, 0);
@@ -674,6 +696,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 continue;
             }
             is_time = b.time; is_norm = hn; is_mat = hmat;
+            if (TEX) is_kd = hit_kd(P, S, b, hmat);
             fl &= ~4;                                              // hit point / normal = at(ray, is_time), is_norm
             if (cur.depth > 0) {                                   // scene.cu:109-121
                 if (cur.in_obj) {
@@ -712,7 +735,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         }
         if (light_done) {
             const V4 inc = (S.lights[li].type == 0) ? da * att : att;   // PointLight: dist_atten * attenuate()
-            summed = summed + phong(S.mats[is_mat], is_norm, inc, cur.ray.d, dtl);
+            const DMat& mm = S.mats[is_mat];
+            summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
             li++;
             st = ST_LIGHT;
         }
@@ -761,7 +785,8 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // counters in VGPRs, so frames without statistics use a kernel without them.
 // MODE bit 2 (PARK): park integrator state in LDS during queries (trace_sample); needs
 // PARK_FIELDS x 4 B x TRACE_BLOCK_P of LDS beside the BVH image.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4;
+// MODE bit 3 (TEX): textured shading (hit_kd), generic frame depth only.
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -770,6 +795,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
+    constexpr bool TEX = (MODE & M_TEX) != 0;
     float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
@@ -814,7 +840,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             }
             if (rd == 0) request(qi);                          // next ticket, in flight during the trace
             const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
             if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
@@ -1080,6 +1106,8 @@ struct rt_scene {
     unsigned long long* d_stats = nullptr;
     uint32_t* d_canvas = nullptr;
     int* d_dbg = nullptr;
+    float4* d_atlas = nullptr;                   // atlas texels (float4, byte / 255)
+    bool atlas_dirty = false;
     void* d_out[4] = {nullptr, nullptr, nullptr, nullptr};   // staging for host_outputs
     std::vector<hipEvent_t> tev;      // timing=1 event triples (pool)
     size_t tev_used = 0;
@@ -1107,6 +1135,8 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
 }
 
 int upload_inst4(rt_scene* s);
+void free_atlas(rt_scene* s);
+int ensure_atlas(rt_scene* s);
 
 int upload(rt_scene* s) {
     if (s->uploaded) return RT_OK;
@@ -1161,6 +1191,29 @@ int upload_inst4(rt_scene* s) {
         v[i] = make_float4(d.pose.p.x, d.pose.p.y, d.pose.p.z, fw);
     }
     if (!v.empty()) HIPCHK(hipMemcpy(s->d_inst4, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+// Atlas -> float4 texels (byte / 255, as assets.cc:61-81) in HBM; the reference's CUDA
+// texture (gputils TextureBuffer4D, alloc.h:24-80: point sampling, clamp) is sampled
+// explicitly by hit_kd, since gfx950 has no texture units.
+void free_atlas(rt_scene* s) {
+    if (s->d_atlas) (void)hipFree(s->d_atlas);
+    s->d_atlas = nullptr;
+}
+int ensure_atlas(rt_scene* s) {
+    const rt::Scene& h = s->h;
+    if (h.atlas_rgba.empty()) return fail(RT_ERR_STATE, "textured rendering needs an atlas: rt_scene_load_atlas / rt_scene_set_atlas");
+    if (!s->atlas_dirty && s->d_atlas) return RT_OK;
+    free_atlas(s);
+    const size_t n = (size_t)h.atlas_w * h.atlas_h;
+    std::vector<float4> texels(n);
+    for (size_t i = 0; i < n; i++)
+        texels[i] = make_float4((float)h.atlas_rgba[4 * i] / 255, (float)h.atlas_rgba[4 * i + 1] / 255,
+                                (float)h.atlas_rgba[4 * i + 2] / 255, (float)h.atlas_rgba[4 * i + 3] / 255);
+    HIPCHK(hipMalloc((void**)&s->d_atlas, n * sizeof(float4)));
+    HIPCHK(hipMemcpy(s->d_atlas, texels.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+    s->atlas_dirty = false;
     return RT_OK;
 }
 
@@ -1234,6 +1287,11 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.spp_off = s->d_spp;
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
     P.stats = want_stats ? s->d_stats : nullptr; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
+    if (o.textures) {
+        int r;
+        if ((r = ensure_atlas(s)) != RT_OK) return r;
+        P.atlas = s->d_atlas; P.atlas_w = s->h.atlas_w; P.atlas_h = s->h.atlas_h;
+    }
     SceneView S = view_of(s, o.use_bvh != 0);
     // sample-parallel mapping: L lanes per pixel (one sample each per round), 64/L pixels per wave
     P.lanes_per_px = std::min(o.spp, 64);
@@ -1258,9 +1316,17 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, false, 2>, (const void*)trace_kernel<NG, false, 3>},
         {(const void*)trace_kernel<NG, true, 0>, (const void*)trace_kernel<NG, true, 1>,
          (const void*)trace_kernel<NG, true, 2>, (const void*)trace_kernel<NG, true, 3>}};
+    static const void* const textured[2][4] = {
+        {(const void*)trace_kernel<NG, false, 8>, (const void*)trace_kernel<NG, false, 9>,
+         (const void*)trace_kernel<NG, false, 10>, (const void*)trace_kernel<NG, false, 11>},
+        {(const void*)trace_kernel<NG, true, 8>, (const void*)trace_kernel<NG, true, 9>,
+         (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
+    const bool tex = o.textures != 0;
     const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
-    const bool park = mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    if (park) {
+    const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
+    if (tex) {
+        fn = textured[use_lds ? 1 : 0][mode];
+    } else if (park) {
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, M_PARK> : ns <= 2 ? (const void*)trace_kernel<2, true, M_PARK>
                      : (const void*)trace_kernel<NG, true, M_PARK>;
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
@@ -1297,6 +1363,7 @@ void invalidate(rt_scene* s) { s->bvh_valid = false; }
 
 rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
+    free_atlas(this);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
@@ -1378,6 +1445,17 @@ int rt_builder_add_triangle(rt_scene* s, int mesh, int i0, int i1, int i2, const
     s->h.add_triangle(mesh, i0, i1, i2, s->h.add_material(mat_from(mat)));
     return RT_OK;
 }
+int rt_builder_add_triangle_tex(rt_scene* s, int mesh, int i0, int i1, int i2, const float* mat, const float* tex) {
+    CHECK_BUILDING(s);
+    if (!mat || !tex) return fail(RT_ERR_ARG, "null argument");
+    if (mesh < 0 || mesh >= (int)s->h.meshes.size()) return fail(RT_ERR_ARG, "mesh index out of range");
+    int nv = (int)s->h.verts.size();
+    if (i0 < 0 || i1 < 0 || i2 < 0 || i0 >= nv || i1 >= nv || i2 >= nv) return fail(RT_ERR_ARG, "vertex index out of range");
+    rt::TexDesc t;
+    t.has = 1; t.tx = tex[0]; t.ty = tex[1]; t.ux = tex[2]; t.uy = tex[3]; t.vx = tex[4]; t.vy = tex[5];
+    s->h.add_triangle(mesh, i0, i1, i2, s->h.add_material(mat_from(mat)), t);
+    return RT_OK;
+}
 int rt_builder_add_trans(rt_scene* s, int mesh, int* trans) {
     CHECK_BUILDING(s);
     if (mesh < 0 || mesh >= (int)s->h.meshes.size()) return fail(RT_ERR_ARG, "mesh index out of range");
@@ -1405,6 +1483,13 @@ int rt_builder_build_cube(rt_scene* s, float scale, const float* mat, int* mesh)
     CHECK_BUILDING(s);
     if (!mat) return fail(RT_ERR_ARG, "null material");
     int m = s->h.build_cube(scale, mat_from(mat));
+    if (mesh) *mesh = m;
+    return RT_OK;
+}
+int rt_builder_build_cube_tex(rt_scene* s, float scale, const float* mat, const float* tile, int* mesh) {
+    CHECK_BUILDING(s);
+    if (!mat || !tile) return fail(RT_ERR_ARG, "null argument");
+    int m = s->h.build_cube(scale, mat_from(mat), tile);
     if (mesh) *mesh = m;
     return RT_OK;
 }
@@ -1478,6 +1563,15 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
         case RT_EXPORT_ENV:
             f = {h.dist_atten.x, h.dist_atten.y, h.dist_atten.z, h.ambience.x, h.ambience.y, h.ambience.z, h.ambience.w};
             break;
+        case RT_EXPORT_TEXCOORDS:
+            for (auto& t : h.tris) f.insert(f.end(), {(float)t.tex.has, t.tex.tx, t.tex.ty, t.tex.ux, t.tex.uy, t.tex.vx, t.tex.vy});
+            break;
+        case RT_EXPORT_ATLAS: {
+            const size_t n = h.atlas_rgba.size();
+            if (!dst || cap < (int64_t)n) return fail(RT_ERR_ARG, "destination too small");
+            if (n) memcpy(dst, h.atlas_rgba.data(), n);
+            return RT_OK;
+        }
         default: return fail(RT_ERR_ARG, "unknown export");
     }
     size_t bytes = f.size() * 4 + iv.size() * 4;
@@ -1528,6 +1622,40 @@ int rt_env_set(rt_scene* s, const float* amb, const float* da, int depth) {
     if (amb) s->h.ambience = v4(amb[0], amb[1], amb[2], amb[3]);
     if (da) s->h.dist_atten = v3(da[0], da[1], da[2]);
     s->h.depth = depth;
+    return RT_OK;
+}
+
+int rt_scene_set_atlas(rt_scene* s, const uint8_t* rgba8, int w, int h) {
+    if (!s) return fail(RT_ERR_ARG, "null scene");
+    if (!rgba8 || w <= 0 || h <= 0 || w > 16384 || h > 16384) return fail(RT_ERR_ARG, "bad atlas image");
+    s->h.atlas_rgba.assign(rgba8, rgba8 + (size_t)w * h * 4);
+    s->h.atlas_w = w; s->h.atlas_h = h;
+    s->atlas_dirty = true;
+    return RT_OK;
+}
+int rt_scene_load_atlas(rt_scene* s, const char* path) {
+    if (!s) return fail(RT_ERR_ARG, "null scene");
+    std::vector<std::string> tries;
+    if (path) tries.push_back(path);
+    else {
+        if (s->h.atlas.empty()) return fail(RT_ERR_STATE, "the scene names no atlas");
+        if (s->h.atlas[0] != '/' && !s->h.base_dir.empty()) tries.push_back(s->h.base_dir + "/" + s->h.atlas);
+        tries.push_back(s->h.atlas);
+    }
+    std::string err;
+    for (const std::string& p : tries) {
+        std::ifstream probe(p, std::ios::binary);
+        if (!probe) { err = p + ": cannot open"; continue; }
+        std::vector<uint8_t> px;
+        int w = 0, h = 0;
+        if (rt::load_png_rgba8(p, &px, &w, &h, &err) != 0) return fail(RT_ERR_PARSE, err);
+        return rt_scene_set_atlas(s, px.data(), w, h);
+    }
+    return fail(RT_ERR_IO, err);
+}
+int rt_scene_atlas_info(const rt_scene* s, int32_t* a) {
+    if (!s || !a) return fail(RT_ERR_ARG, "null argument");
+    a[0] = s->h.atlas_w; a[1] = s->h.atlas_h; a[2] = s->h.atlas_rgba.empty() ? 0 : 1;
     return RT_OK;
 }
 

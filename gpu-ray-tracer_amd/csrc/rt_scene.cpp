@@ -24,6 +24,8 @@
 #include <sstream>
 #include <stdexcept>
 
+#include <zlib.h>
+
 namespace rt {
 using namespace rtm;
 
@@ -175,7 +177,7 @@ class Perlin {
 }  // namespace
 
 // SceneBuilder::build_cube (scene_builder.cu:181-239): 12 triangles, 36 unshared vertices.
-int Scene::build_cube(float scale, const Material& mat) {
+int Scene::build_cube(float scale, const Material& mat, const float* tile) {
     const V3 A = scale * v3(-0.5f, 0.5f, -0.5f), B = scale * v3(0.5f, 0.5f, -0.5f);
     const V3 C = scale * v3(-0.5f, -0.5f, -0.5f), D = scale * v3(0.5f, -0.5f, -0.5f);
     const V3 E = scale * v3(-0.5f, 0.5f, 0.5f), F = scale * v3(0.5f, 0.5f, 0.5f);
@@ -188,9 +190,29 @@ int Scene::build_cube(float scale, const Material& mat) {
                               {&C, &G, &A}, {&A, &G, &E},     // left
                               {&G, &Hh, &E}, {&E, &Hh, &F},   // back
                               {&G, &C, &D}, {&D, &Hh, &G}};   // bottom
-    for (auto& f : faces) {
+    // Texture tile (build-defined): face-local (s, t) in [-scale/2, scale/2] -> the
+    // square [tx, tx+size] x [ty, ty+size] of the atlas, image rows downwards.
+    // Faces in the order above: front/back use (x, y), top/bottom (x, z), right/left (z, y).
+    static const int face_axes[6][2] = {{0, 1}, {0, 2}, {2, 1}, {2, 1}, {0, 1}, {0, 2}};
+    for (int k = 0; k < 12; k++) {
+        const V3* const* f = faces[k];
         int i0 = add_vertex(*f[0]), i1 = add_vertex(*f[1]), i2 = add_vertex(*f[2]);
-        add_triangle(m, i0, i1, i2, mi);
+        TexDesc tex;
+        if (tile) {
+            const int* ax = face_axes[k / 2];
+            auto T = [&](const V3& p, float* o) {
+                const float c[3] = {p.x, p.y, p.z};
+                o[0] = tile[0] + (c[ax[0]] / scale + 0.5f) * tile[2];
+                o[1] = tile[1] + (0.5f - c[ax[1]] / scale) * tile[2];
+            };
+            float t0[2], t1[2], t2[2];
+            T(*f[0], t0); T(*f[1], t1); T(*f[2], t2);
+            tex.has = 1;
+            tex.tx = t0[0]; tex.ty = t0[1];
+            tex.ux = t1[0] - t0[0]; tex.uy = t1[1] - t0[1];
+            tex.vx = t2[0] - t0[0]; tex.vy = t2[1] - t0[1];
+        }
+        add_triangle(m, i0, i1, i2, mi, tex);
     }
     return m;
 }
@@ -250,6 +272,8 @@ int Scene::flatten(std::string* err) {
             d.area = len(pn);                                    // geometry.h:280
             d.inv_area = 1.0f / d.area;
             d.mat = tr.mat;
+            d.tex = tr.tex.has;
+            d.tx = tr.tex.tx; d.ty = tr.tex.ty; d.ux = tr.tex.ux; d.uy = tr.tex.uy; d.vx = tr.tex.vx; d.vy = tr.tex.vy;
             d.n0 = norms[tr.i0]; d.n1 = norms[tr.i1]; d.n2 = norms[tr.i2];
             d_tris.push_back(d);
         }
@@ -293,6 +317,8 @@ int load_cube_world(const std::string& path, int width, int height, Scene* s, st
         if (W <= 0 || H <= 0) throw std::runtime_error("canvas size must be positive");
         if (grid < 0) throw std::runtime_error("grid_size must be >= 0");
         s->atlas = doc.has("atlas") ? doc.at("atlas").str : std::string();
+        const size_t slash = path.find_last_of('/');
+        s->base_dir = slash == std::string::npos ? std::string(".") : path.substr(0, slash);
         s->set_camera(W, H, fov, unit);
 
         const float inv255 = 1.0f / 255;                          // 1.0f / UINT8_MAX
@@ -311,7 +337,12 @@ int load_cube_world(const std::string& path, int width, int height, Scene* s, st
                 if (c.has("Kr")) m.Kr = read_vec4(c.at("Kr"));
                 if (c.has("alpha")) m.alpha = (float)c.at("alpha").number();
                 if (c.has("eta")) m.eta = (float)c.at("eta").number();
-                s->build_cube(.999f, m);
+                // "texture": [tx, ty, size] (build-defined; the reference leaves this key a
+                // TODO, cube_world.cc:79-81, so it changes nothing unless textures are on)
+                float tile[3];
+                const bool tex = c.has("texture") && c.at("texture").arr.size() == 3;
+                if (tex) for (int k = 0; k < 3; k++) tile[k] = (float)c.at("texture").at(k).number();
+                s->build_cube(.999f, m, tex ? tile : nullptr);
             }
         }
         if (doc.has("lights")) {
@@ -362,6 +393,73 @@ void spp_offset(int k, float* dx, float* dy) {
     double u = (double)k * a1, v = (double)k * a2;
     *dx = (float)(u - floor(u));
     *dy = (float)(v - floor(v));
+}
+
+// Atlas PNG (assets.cc:11-57 reads it with libpng; this build uses zlib directly).
+// Supports what the reference's atlas is: 8-bit RGBA (colour type 6) or RGB (2),
+// non-interlaced; RGB gets alpha 255.
+int load_png_rgba8(const std::string& path, std::vector<uint8_t>* out, int* w, int* h, std::string* err) {
+    auto fail = [&](const std::string& m) { if (err) *err = path + ": " + m; return -1; };
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return fail("cannot open");
+    std::vector<uint8_t> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0d, 0x0a, 0x1a, 0x0a};
+    if (d.size() < 8 || memcmp(d.data(), sig, 8) != 0) return fail("not a PNG file");
+    auto be32 = [&](size_t o) { return (uint32_t)d[o] << 24 | (uint32_t)d[o + 1] << 16 | (uint32_t)d[o + 2] << 8 | d[o + 3]; };
+    uint32_t W = 0, H = 0;
+    int depth = 0, ctype = 0, interlace = 0;
+    std::vector<uint8_t> idat;
+    for (size_t o = 8; o + 12 <= d.size();) {
+        const uint32_t n = be32(o);
+        if (o + 12 + (size_t)n > d.size()) return fail("truncated chunk");
+        const std::string type(reinterpret_cast<const char*>(&d[o + 4]), 4);
+        const uint8_t* c = &d[o + 8];
+        if (type == "IHDR" && n >= 13) {
+            W = be32(o + 8); H = be32(o + 12); depth = c[8]; ctype = c[9]; interlace = c[12];
+        } else if (type == "IDAT") {
+            idat.insert(idat.end(), c, c + n);
+        } else if (type == "IEND") {
+            break;
+        }
+        o += 12 + (size_t)n;
+    }
+    if (!W || !H || W > 16384 || H > 16384) return fail("bad image size");
+    if (depth != 8 || (ctype != 6 && ctype != 2) || interlace) return fail("only 8-bit RGB/RGBA non-interlaced PNGs");
+    const int bpp = ctype == 6 ? 4 : 3;
+    const size_t stride = (size_t)W * bpp;
+    std::vector<uint8_t> raw((stride + 1) * H);
+    uLongf raw_len = (uLongf)raw.size();
+    if (uncompress(raw.data(), &raw_len, idat.data(), (uLong)idat.size()) != Z_OK || raw_len != raw.size())
+        return fail("corrupt image data");
+    std::vector<uint8_t> img(stride * H);
+    for (uint32_t y = 0; y < H; y++) {                       // undo the scanline filters (PNG spec 9.2)
+        const uint8_t* src = &raw[y * (stride + 1)];
+        uint8_t* row = &img[y * stride];
+        const uint8_t* up = y ? &img[(y - 1) * stride] : nullptr;
+        for (size_t x = 0; x < stride; x++) {
+            const int a = x >= (size_t)bpp ? row[x - bpp] : 0, b = up ? up[x] : 0;
+            const int c = (up && x >= (size_t)bpp) ? up[x - bpp] : 0;
+            int v = src[1 + x];
+            switch (src[0]) {
+                case 0: break;
+                case 1: v += a; break;
+                case 2: v += b; break;
+                case 3: v += (a + b) / 2; break;
+                case 4: {
+                    const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+                    v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+                    break;
+                }
+                default: return fail("bad filter type");
+            }
+            row[x] = (uint8_t)v;
+        }
+    }
+    out->assign((size_t)W * H * 4, 255);
+    for (size_t i = 0; i < (size_t)W * H; i++)
+        for (int k = 0; k < bpp; k++) (*out)[4 * i + k] = img[i * bpp + k];
+    *w = (int)W; *h = (int)H;
+    return 0;
 }
 
 }  // namespace rt

@@ -22,7 +22,11 @@ struct Material {                        // include/rayprimitives/material.h:14-
 };
 
 struct MeshDesc { rtm::Q rot{0, 0, 0, 1}; rtm::V3 pos{0, 0, 0}; std::vector<int> tris; };
-struct TriDesc { int i0, i1, i2, mat; };
+// rprimitives::TextureCoords (texture_coords.h:12-29): atlas texel of a hit with
+// barycentric weights (u, v) of vertices 1 and 2 = (tx, ty) + u * (ux, uy) + v * (vx, vy).
+// Build-defined: the reference stores these but never samples them (phong.cu:18-23).
+struct TexDesc { int has = 0; float tx = 0, ty = 0, ux = 0, uy = 0, vx = 0, vy = 0; };
+struct TriDesc { int i0, i1, i2, mat; TexDesc tex; };
 struct InstDesc { rtm::Q rot{0, 0, 0, 1}; rtm::V3 pos{0, 0, 0}; int mesh; };
 struct LightDesc { int type; rtm::V3 v; rtm::V4 col; };   // 0 point(pos), 1 directional(normalized dir)
 
@@ -34,12 +38,14 @@ struct CameraDesc {
 };
 
 // ---- device-ready records (all plain-old-data, 16-byte aligned) ----
-struct alignas(16) DTri {              // 96 B: the plane filter's (pn, a) first (one 32-B scalar load)
+struct alignas(16) DTri {              // 128 B: the plane filter's (pn, a) first (one 32-B scalar load)
     rtm::V3 pn, a, b, c;               // normalized plane normal, vertices (mesh-local)
     float area;                        // |cross(b-a, c-a)|
     float inv_area;                    // fl(1/area): only used by the filtered test's estimate
     rtm::V3 n0, n1, n2;                // vertex normals (generate_normals)
-    int mat, pad;
+    int mat, tex;                      // tex: 1 if the texture coordinates below are set
+    float tx, ty, ux, uy, vx, vy;      // TexDesc (textured shading mode only)
+    int pad[2];
 };
 struct alignas(16) DMesh { rtm::Pose pose; int tri_begin, tri_count, pad[2]; };
 struct alignas(16) DInst { rtm::Pose pose; int mesh, pad[3]; };
@@ -54,7 +60,10 @@ struct DCamera {                       // Camera::at (camera.cu:33-42) with the 
 
 struct Scene {
     // builder state (SceneBuilder)
-    std::string atlas;
+    std::string atlas;                 // atlas path as given (JSON "atlas" / SceneBuilder{atlas})
+    std::string base_dir;              // directory of the scene file (atlas paths resolve here first)
+    std::vector<uint8_t> atlas_rgba;   // RGBA8 texels, row-major (empty: no atlas loaded)
+    int atlas_w = 0, atlas_h = 0;
     std::vector<rtm::V3> verts, norms;
     std::vector<TriDesc> tris;
     std::vector<Material> mats;
@@ -79,12 +88,13 @@ struct Scene {
     int add_vertex(rtm::V3 v) { verts.push_back(v); return (int)verts.size() - 1; }
     int create_mesh(rtm::V3 pos, rtm::Q rot) { MeshDesc m; m.pos = pos; m.rot = rot; meshes.push_back(m); return (int)meshes.size() - 1; }
     int add_material(const Material& m) { mats.push_back(m); return (int)mats.size() - 1; }
-    void add_triangle(int mesh, int i0, int i1, int i2, int mat) {
-        tris.push_back(TriDesc{i0, i1, i2, mat});
+    void add_triangle(int mesh, int i0, int i1, int i2, int mat, const TexDesc& tex = TexDesc{}) {
+        tris.push_back(TriDesc{i0, i1, i2, mat, tex});
         meshes[mesh].tris.push_back((int)tris.size() - 1);
     }
     int add_trans(int mesh) { InstDesc t; t.mesh = mesh; insts.push_back(t); return (int)insts.size() - 1; }
-    int build_cube(float scale, const Material& mat);
+    // tile (optional, build-defined): {tx, ty, size} maps every face onto that atlas square
+    int build_cube(float scale, const Material& mat, const float* tile = nullptr);
     void add_point_light(rtm::V3 pos, rtm::V4 col) { points.push_back(LightDesc{0, pos, col}); }
     void add_directional_light(rtm::V3 dir, rtm::V4 col) { dirs.push_back(LightDesc{1, rtm::normalized(dir), col}); }
 
@@ -96,6 +106,10 @@ struct Scene {
 
 // worldN.json -> Scene (cube_world.cc:38-191).  width/height > 0 override the JSON.
 int load_cube_world(const std::string& path, int width, int height, Scene* out, std::string* err);
+
+// 8-bit RGBA/RGB non-interlaced PNG -> RGBA8 (the atlas format assets.cc:11-57 reads
+// through libpng; here with zlib).  Returns 0 or -1 with *err set.
+int load_png_rgba8(const std::string& path, std::vector<uint8_t>* out, int* w, int* h, std::string* err);
 
 // Build-defined spp sample offsets: R2 sequence in IEEE double, k=0 -> (0,0).
 void spp_offset(int k, float* dx, float* dy);

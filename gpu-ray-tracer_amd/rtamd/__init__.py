@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("RTAMD_LIB", os.path.join(PKG, "librt_amd.so"))
 
 RT_OK, RT_ERR_ARG, RT_ERR_IO, RT_ERR_PARSE, RT_ERR_HIP, RT_ERR_STATE, RT_ERR_NODEV, RT_ERR_LIMIT = 0, -1, -2, -3, -4, -5, -6, -7
 EXPORTS = {"vertices": 0, "normals": 1, "tris": 2, "materials": 3, "instances": 4, "inst_mesh": 5,
-           "lights": 6, "camera": 7, "env": 8}
+           "lights": 6, "camera": 7, "env": 8, "texcoords": 9}
 
 # Every symbol include/rt_amd.h declares (checked by tests/test_abi.py).
 SYMBOLS = [
@@ -34,6 +34,8 @@ SYMBOLS = [
     "rt_camera_set", "rt_camera_translate", "rt_camera_rotate", "rt_camera_axes", "rt_env_set",
     "rt_render_opts_default", "rt_render", "rt_update_scene", "rt_canvas_read", "rt_canvas_host_ptr",
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
+    "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
+    "rt_scene_atlas_info",
 ]
 
 
@@ -48,7 +50,8 @@ class RenderOpts(ctypes.Structure):
                 ("row0", ctypes.c_int), ("row_step", ctypes.c_int), ("compact", ctypes.c_int),
                 ("kernel_dim", ctypes.c_int), ("stream", ctypes.c_void_p), ("rgba", ctypes.c_void_p),
                 ("radiance", ctypes.c_void_p), ("hit_inst", ctypes.c_void_p), ("hit_tri", ctypes.c_void_p),
-                ("sync", ctypes.c_int), ("host_outputs", ctypes.c_int), ("timing", ctypes.c_int)]
+                ("sync", ctypes.c_int), ("host_outputs", ctypes.c_int), ("timing", ctypes.c_int),
+                ("textures", ctypes.c_int)]
 
 
 class Stats(ctypes.Structure):
@@ -82,6 +85,11 @@ def lib():
     L.rt_builder_add_trans.argtypes = [vp, ip, ctypes.POINTER(ip)]
     L.rt_builder_set_trans.argtypes = [vp, ip, vp, vp]
     L.rt_builder_build_cube.argtypes = [vp, ctypes.c_float, vp, ctypes.POINTER(ip)]
+    L.rt_builder_build_cube_tex.argtypes = [vp, ctypes.c_float, vp, vp, ctypes.POINTER(ip)]
+    L.rt_builder_add_triangle_tex.argtypes = [vp, ip, ip, ip, ip, vp, vp]
+    L.rt_scene_set_atlas.argtypes = [vp, vp, ip, ip]
+    L.rt_scene_load_atlas.argtypes = [vp, ctypes.c_char_p]
+    L.rt_scene_atlas_info.argtypes = [vp, vp]
     L.rt_builder_add_point_light.argtypes = [vp, vp, vp]
     L.rt_builder_add_directional_light.argtypes = [vp, vp, vp]
     L.rt_builder_finish.argtypes = [vp, ip, ip, ctypes.c_float, ctypes.c_float, vp, vp, vp, vp, ip]
@@ -203,10 +211,40 @@ class Scene:
         _check(lib().rt_builder_set_trans(self._h, t, _ptr(None if pos is None else _f(pos, 3)),
                                           _ptr(None if quat is None else _f(quat, 4))))
 
-    def build_cube(self, scale, mat):
+    def build_cube(self, scale, mat, tile=None):
+        """tile=(tx, ty, size): every face mapped onto that atlas square (textured mode)."""
         i = ctypes.c_int()
-        _check(lib().rt_builder_build_cube(self._h, scale, _ptr(_f(mat, 26)), ctypes.byref(i)))
+        if tile is None:
+            _check(lib().rt_builder_build_cube(self._h, scale, _ptr(_f(mat, 26)), ctypes.byref(i)))
+        else:
+            _check(lib().rt_builder_build_cube_tex(self._h, scale, _ptr(_f(mat, 26)), _ptr(_f(tile, 3)),
+                                                   ctypes.byref(i)))
         return i.value
+
+    def add_triangle_tex(self, mesh, i0, i1, i2, mat, tex6):
+        _check(lib().rt_builder_add_triangle_tex(self._h, mesh, i0, i1, i2, _ptr(_f(mat, 26)), _ptr(_f(tex6, 6))))
+
+    # ---- texture atlas (textured shading mode) ----
+    def load_atlas(self, path=None):
+        _check(lib().rt_scene_load_atlas(self._h, None if path is None else path.encode()))
+
+    def set_atlas(self, rgba8):
+        a = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        assert a.ndim == 3 and a.shape[2] == 4
+        _check(lib().rt_scene_set_atlas(self._h, _ptr(a), a.shape[1], a.shape[0]))
+
+    def atlas(self):
+        """The loaded atlas as (H, W, 4) uint8 (empty array if none)."""
+        a = self.atlas_info()
+        out = np.zeros((a["height"], a["width"], 4), np.uint8)
+        if out.size:
+            _check(lib().rt_scene_export(self._h, 10, _ptr(out), out.nbytes))
+        return out
+
+    def atlas_info(self):
+        v = np.zeros(3, np.int32)
+        _check(lib().rt_scene_atlas_info(self._h, _ptr(v)))
+        return {"width": int(v[0]), "height": int(v[1]), "loaded": bool(v[2])}
 
     def add_point_light(self, pos, col):
         _check(lib().rt_builder_add_point_light(self._h, _ptr(_f(pos, 3)), _ptr(_f(col, 4))))
@@ -242,7 +280,8 @@ class Scene:
         shapes = {"vertices": ((i["n_vertices"], 3), np.float32), "normals": ((i["n_vertices"], 3), np.float32),
                   "tris": ((i["n_tris"], 4), np.int32), "materials": ((i["n_mats"], 26), np.float32),
                   "instances": ((i["n_instances"], 7), np.float32), "inst_mesh": ((i["n_instances"],), np.int32),
-                  "lights": ((i["n_lights"], 8), np.float32), "camera": ((21,), np.float32), "env": ((7,), np.float32)}
+                  "lights": ((i["n_lights"], 8), np.float32), "camera": ((21,), np.float32), "env": ((7,), np.float32),
+                  "texcoords": ((i["n_tris"], 7), np.float32)}
         shp, dt = shapes[what]
         a = np.zeros(shp, dt)
         _check(lib().rt_scene_export(self._h, EXPORTS[what], _ptr(a), a.nbytes))
@@ -280,14 +319,14 @@ class Scene:
 
     # ---- rendering ----
     def render(self, spp=1, use_bvh=True, rebuild_bvh=True, row0=0, row_step=1, compact=False,
-               want=("rgba",), stats=True):
+               want=("rgba",), stats=True, textures=False):
         """Render to host numpy arrays (outputs staged through device buffers)."""
         W, H = self.width, self.height
         rows = len(range(row0, H, row_step)) if compact else H
         o = RenderOpts()
         lib().rt_render_opts_default(ctypes.byref(o))
         o.spp, o.use_bvh, o.rebuild_bvh, o.row0, o.row_step, o.compact = spp, int(use_bvh), int(rebuild_bvh), row0, row_step, int(compact)
-        o.host_outputs, o.sync = 1, 1
+        o.host_outputs, o.sync, o.textures = 1, 1, int(textures)
         out = {}
         if "rgba" in want:
             out["rgba"] = np.zeros((rows, W), np.uint32)
@@ -309,13 +348,13 @@ class Scene:
 
     def render_device(self, spp=1, use_bvh=True, rebuild_bvh=True, row0=0, row_step=1, compact=True,
                       rgba_ptr=None, radiance_ptr=None, hit_inst_ptr=None, hit_tri_ptr=None, stream=None,
-                      sync=False, stats=False, timing=False):
+                      sync=False, stats=False, timing=False, textures=False):
         """Render into caller-owned DEVICE buffers (e.g. torch tensors' data_ptr())."""
         o = RenderOpts()
         lib().rt_render_opts_default(ctypes.byref(o))
         o.spp, o.use_bvh, o.rebuild_bvh, o.row0, o.row_step, o.compact = spp, int(use_bvh), int(rebuild_bvh), row0, row_step, int(compact)
         o.rgba, o.radiance, o.hit_inst, o.hit_tri = rgba_ptr, radiance_ptr, hit_inst_ptr, hit_tri_ptr
-        o.stream, o.sync, o.host_outputs, o.timing = stream, int(sync), 0, int(timing)
+        o.stream, o.sync, o.host_outputs, o.timing, o.textures = stream, int(sync), 0, int(timing), int(textures)
         st = Stats()
         _check(lib().rt_render(self._h, ctypes.byref(o), ctypes.byref(st) if stats else None))
         return st.as_dict() if stats else None

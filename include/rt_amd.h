@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -56,9 +56,16 @@ int rt_builder_add_vertex(rt_scene* s, float x, float y, float z, int* idx);
 int rt_builder_create_mesh(rt_scene* s, const float pos3[3], const float quat4[4], int* mesh);
 /* material26: Ke[4] Ka[4] Kd[4] Ks[4] Kt[4] Kr[4] alpha eta (material.h:14-31) */
 int rt_builder_add_triangle(rt_scene* s, int mesh, int i0, int i1, int i2, const float material26[26]);
+/* add_triangle with rprimitives::TextureCoords (texture_coords.h:12-29): tex6 = {tx, ty, ux, uy, vx, vy};
+ * a hit with barycentric weights (u, v) of vertices i1, i2 reads atlas texel (tx, ty) + u (ux, uy) + v (vx, vy)
+ * in the textured shading mode (build-defined: the reference never samples, phong.cu:18-23). */
+int rt_builder_add_triangle_tex(rt_scene* s, int mesh, int i0, int i1, int i2, const float material26[26],
+                                const float tex6[6]);
 int rt_builder_add_trans(rt_scene* s, int mesh, int* trans);
 int rt_builder_set_trans(rt_scene* s, int trans, const float pos3[3], const float quat4[4]);  /* either may be NULL */
 int rt_builder_build_cube(rt_scene* s, float scale, const float material26[26], int* mesh);
+/* build_cube with every face mapped onto the atlas square tile3 = {tx, ty, size} (texels). */
+int rt_builder_build_cube_tex(rt_scene* s, float scale, const float material26[26], const float tile3[3], int* mesh);
 int rt_builder_add_point_light(rt_scene* s, const float pos3[3], const float col4[4]);
 int rt_builder_add_directional_light(rt_scene* s, const float dir3[3], const float col4[4]);
 /* Canvas + Camera (camera.cu:6-9) + Environment (environment.h:19-93); finalises the builder. */
@@ -66,11 +73,24 @@ int rt_builder_finish(rt_scene* s, int width, int height, float fov_radians, flo
                       const float cam_pos3[3], const float cam_quat4[4],
                       const float dist_atten3[3], const float ambience4[4], int depth);
 
+/* ---- texture atlas (assets.cc:61-81, gputils TextureBuffer4D alloc.h:24-80) ----
+ * Texels are float RGBA = byte / 255 in HBM, point-sampled with clamp addressing as the
+ * reference's texture object (gfx950 has no texture units).  Only read when
+ * rt_render_opts.textures = 1. */
+int rt_scene_set_atlas(rt_scene* s, const uint8_t* rgba8, int width, int height);
+/* Decode an 8-bit RGB/RGBA PNG.  png_path NULL: the scene's own atlas entry (JSON "atlas"
+ * or SceneBuilder{atlas}), resolved against the scene file's directory, then the CWD. */
+int rt_scene_load_atlas(rt_scene* s, const char* png_path);
+/* atlas3 = {width, height, loaded} */
+int rt_scene_atlas_info(const rt_scene* s, int32_t atlas3[3]);
+
 /* info10 = {W, H, n_vertices, n_tris, n_meshes, n_instances, n_lights, n_point_lights, depth, n_materials} */
 int rt_scene_info(const rt_scene* s, int32_t info10[10]);
 /* Host copies of the scene arrays (layouts as in oracle/rt_oracle.h) for parity checks. */
 enum { RT_EXPORT_VERTICES = 0, RT_EXPORT_NORMALS = 1, RT_EXPORT_TRIS = 2, RT_EXPORT_MATERIALS = 3,
-       RT_EXPORT_INSTANCES = 4, RT_EXPORT_INST_MESH = 5, RT_EXPORT_LIGHTS = 6, RT_EXPORT_CAMERA = 7, RT_EXPORT_ENV = 8 };
+       RT_EXPORT_INSTANCES = 4, RT_EXPORT_INST_MESH = 5, RT_EXPORT_LIGHTS = 6, RT_EXPORT_CAMERA = 7, RT_EXPORT_ENV = 8,
+       RT_EXPORT_TEXCOORDS = 9,   /* per triangle float7 {has, tx, ty, ux, uy, vx, vy} */
+       RT_EXPORT_ATLAS = 10 };    /* atlas RGBA8 bytes, width*height*4 (rt_scene_atlas_info) */
 int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t dst_bytes);
 
 /* ---- camera / environment (entity.h:49-74, environment.h:30-44) ---- */
@@ -99,6 +119,9 @@ typedef struct rt_render_opts {
     int host_outputs;   /* 1: rgba/radiance/hit_* are HOST pointers; results are copied back (implies sync) */
     int timing;         /* 1: record device events around the BVH build and the trace kernel on the
                            launch stream (no sync); totals via rt_timing_collect */
+    int textures;       /* 1: textured shading (build-defined, parity-unpinned): the diffuse colour of a
+                           hit on a triangle with texture coordinates is its atlas texel instead of Kd
+                           (the TODO branch of phong.cu:18-23).  0 (default) = the reference. */
 } rt_render_opts;
 
 typedef struct rt_stats {

@@ -258,7 +258,10 @@ struct Material { V4 Ke{}, Ka{}, Kd{}, Ks{}, Kt{}, Kr{}; float alpha = 0, eta = 
 inline bool reflective(const Material& m) { return m.Kr.x > 0.0f || m.Kr.y > 0.0f || m.Kr.z > 0.0f || m.Kr.w > 0.0f; }
 inline bool refractive(const Material& m) { return m.Kt.x > 0.0f || m.Kt.y > 0.0f || m.Kt.z > 0.0f || m.Kt.w > 0.0f; }
 
-struct Tri { int i0, i1, i2; int mat; };
+// TextureCoords (texture_coords.h:12-29) of the build-defined textured mode (the
+// reference never samples them, phong.cu:18-23): texel = t + u*U + v*V
+struct Tex { int has = 0; float tx = 0, ty = 0, ux = 0, uy = 0, vx = 0, vy = 0; };
+struct Tri { int i0, i1, i2; int mat; Tex tex; };
 struct Mesh { Entity e; int begin, count; };
 struct Inst { Entity e; int mesh; };
 struct Light { int type; V3 v; V4 col; };   // type 0 point (pos), 1 directional (normalized dir)
@@ -280,6 +283,9 @@ struct orc_scene {
     V4 ambience{0, 0, 0, 0};
     int depth = 0;
     Camera cam;
+    std::vector<uint8_t> atlas;      // textured mode (build extension): RGBA8 atlas
+    int atlas_w = 0, atlas_h = 0;
+    int textures = 0;
 };
 
 namespace {
@@ -374,7 +380,10 @@ struct Perlin {
 };
 
 // SceneBuilder::build_cube (scene_builder.cu:181-239)
-void build_cube(orc_scene& s, float scale, const Material& mat) {
+// tile (build extension): {tx, ty, size}: face-local (s, t) in [-scale/2, scale/2] ->
+// [tx, tx+size] x [ty, ty+size], image rows downwards; front/back faces use (x, y),
+// top/bottom (x, z), right/left (z, y) -- the build's documented mapping.
+void build_cube(orc_scene& s, float scale, const Material& mat, const float* tile = nullptr) {
     V3 A = mul(scale, v3(-0.5f, 0.5f, -0.5f)), B = mul(scale, v3(0.5f, 0.5f, -0.5f));
     V3 C = mul(scale, v3(-0.5f, -0.5f, -0.5f)), D = mul(scale, v3(0.5f, -0.5f, -0.5f));
     V3 E = mul(scale, v3(-0.5f, 0.5f, 0.5f)), F = mul(scale, v3(0.5f, 0.5f, 0.5f));
@@ -383,10 +392,23 @@ void build_cube(orc_scene& s, float scale, const Material& mat) {
     Mesh m; m.e = Entity{Quat{0, 0, 0, 1}, v3(0, 0, 0)}; m.begin = (int)s.tris.size(); m.count = 0;
     const V3* faces[12][3] = {{&D, &A, &B}, {&C, &A, &D}, {&A, &E, &B}, {&E, &F, &B}, {&D, &B, &Hh}, {&B, &F, &Hh},
                               {&C, &G, &A}, {&A, &G, &E}, {&G, &Hh, &E}, {&E, &Hh, &F}, {&G, &C, &D}, {&D, &Hh, &G}};
-    for (auto& f : faces) {
+    static const int axes[6][2] = {{0, 1}, {0, 2}, {2, 1}, {2, 1}, {0, 1}, {0, 2}};
+    for (int k = 0; k < 12; k++) {
+        const V3* const* f = faces[k];
         Tri t; int base = (int)s.verts.size();
         s.verts.push_back(*f[0]); s.verts.push_back(*f[1]); s.verts.push_back(*f[2]);
         t.i0 = base; t.i1 = base + 1; t.i2 = base + 2; t.mat = mi;
+        if (tile) {
+            float c[3][2];
+            for (int j = 0; j < 3; j++) {
+                const float p[3] = {f[j]->x, f[j]->y, f[j]->z};
+                c[j][0] = tile[0] + (p[axes[k / 2][0]] / scale + 0.5f) * tile[2];
+                c[j][1] = tile[1] + (0.5f - p[axes[k / 2][1]] / scale) * tile[2];
+            }
+            t.tex.has = 1; t.tex.tx = c[0][0]; t.tex.ty = c[0][1];
+            t.tex.ux = c[1][0] - c[0][0]; t.tex.uy = c[1][1] - c[0][1];
+            t.tex.vx = c[2][0] - c[0][0]; t.tex.vy = c[2][1] - c[0][1];
+        }
         s.tris.push_back(t); m.count++;
     }
     s.meshes.push_back(m);
@@ -442,7 +464,10 @@ void load_cube_world(orc_scene& s, const JV& doc, int w_over, int h_over) {
             if (c.has("Kr")) m.Kr = read_vec4(c["Kr"]);
             if (c.has("alpha")) m.alpha = (float)c["alpha"].num;
             if (c.has("eta")) m.eta = (float)c["eta"].num;
-            build_cube(s, .999f, m);
+            float tile[3];
+            const bool tx = c.has("texture") && c["texture"].arr.size() == 3;
+            if (tx) for (int k = 0; k < 3; k++) tile[k] = (float)c["texture"][k].num;
+            build_cube(s, .999f, m, tx ? tile : nullptr);
         }
     }
     std::vector<Light> pts, dirs;
@@ -676,9 +701,9 @@ V4 shine(const Ctx& x, const Light& L, V3 hit_pos, V3& dir_to_light) {       // 
     return attenuate(x, L, make_ray(hit_pos, dir_to_light), INFINITY);
 }
 inline float fmax_std(float a, float b) { return (a < b) ? b : a; }          // std::max semantics
-V4 phong(const Material& m, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) { // phong.cu:14-33
+V4 phong(const Material& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) { // phong.cu:14-33
     float nd = fmax_std(dot(to_light, nrm), 0.0f);
-    V4 diffuse = smul4(nd, m.Kd);
+    V4 diffuse = smul4(nd, kd);
     V3 reflected = reflect(neg(to_light), nrm);
     float rd = dot(neg(reflected), ray_dir);
     V4 specular = smul4(powf(fmax_std(rd, 0.0f), m.alpha), m.Ks);
@@ -687,11 +712,21 @@ V4 phong(const Material& m, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) { // p
 V4 illuminate(const Ctx& x, const Ray& org, const Isect& is) {              // phong.cu:42-53 / :58-66
     const orc_scene& s = *x.s;
     const Material& m = s.mats[is.mat];
+    V4 kd = m.Kd;                                                            // the reference
+    const Tri& ht = s.tris[is.tri];
+    if (s.textures && ht.tex.has && !s.atlas.empty()) {                      // build extension: point-sampled texel
+        const float xf = (ht.tex.tx + is.u * ht.tex.ux) + is.v * ht.tex.vx;
+        const float yf = (ht.tex.ty + is.u * ht.tex.uy) + is.v * ht.tex.vy;
+        const int ix = (int)std::fmin(std::fmax(xf, 0.0f), (float)(s.atlas_w - 1));
+        const int iy = (int)std::fmin(std::fmax(yf, 0.0f), (float)(s.atlas_h - 1));
+        const uint8_t* px = &s.atlas[4 * ((size_t)iy * s.atlas_w + ix)];
+        kd = V4{(float)px[0] / 255, (float)px[1] / 255, (float)px[2] / 255, (float)px[3] / 255};
+    }
     V4 sum = add4(m.Ke, mul4(m.Ka, s.ambience));                             // org_light (phong.cu:36-39)
     for (const Light& L : s.lights) {
         V3 dtl;
         V4 inc = shine(x, L, ray_at(org, is.time), dtl);
-        sum = add4(sum, phong(m, is.norm, inc, org.d, dtl));
+        sum = add4(sum, phong(m, kd, is.norm, inc, org.d, dtl));
     }
     return sum;
 }
@@ -876,6 +911,18 @@ int orc_load(const char* path, int width, int height, orc_scene** out) {
 }
 
 void orc_free(orc_scene* s) { delete s; }
+
+int orc_set_atlas(orc_scene* s, const uint8_t* rgba8, int w, int h) {
+    if (!s || !rgba8 || w <= 0 || h <= 0) return -1;
+    s->atlas.assign(rgba8, rgba8 + (size_t)w * h * 4);
+    s->atlas_w = w; s->atlas_h = h;
+    return 0;
+}
+int orc_set_textures(orc_scene* s, int on) {
+    if (!s) return -1;
+    s->textures = on ? 1 : 0;
+    return 0;
+}
 
 int orc_scene_counts(const orc_scene* s, int32_t* c) {
     c[0] = s->W; c[1] = s->H; c[2] = (int)s->verts.size(); c[3] = (int)s->tris.size(); c[4] = (int)s->meshes.size();

@@ -36,6 +36,11 @@ enum { ORC_SEM_GPU = 0,   /* renv::gpu::propagate_ray (scene.cu:92-188) — the 
 /* Load a worldN.json (cube_world.cc:38-191).  width/height <= 0 keep the JSON's values. */
 int orc_load(const char* json_path, int width, int height, orc_scene** out);
 void orc_free(orc_scene* s);
+/* Build extension (not in the reference): textured shading -- a hit on a triangle with
+ * TextureCoords takes its diffuse colour from the point-sampled atlas texel (byte/255),
+ * JSON cubes' "texture": [tx, ty, size] map every face onto that square. */
+int orc_set_atlas(orc_scene* s, const uint8_t* rgba8, int width, int height);
+int orc_set_textures(orc_scene* s, int on);
 const char* orc_last_error(void);
 
 /* Scene introspection: counts = {W, H, n_vertices, n_tris, n_meshes, n_instances, n_lights, n_point, depth, n_mats} */

@@ -42,6 +42,8 @@ class Oracle:
         L.orc_scene_instances.argtypes = [ctypes.c_void_p, _f, _i]
         L.orc_scene_camera.argtypes = [ctypes.c_void_p, _f, _f]
         L.orc_spp_offset.argtypes = [ctypes.c_int, _f, _f]
+        L.orc_set_atlas.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.orc_set_textures.argtypes = [ctypes.c_void_p, ctypes.c_int]
         self.L = L
 
     # -- scenes ---------------------------------------------------------------
@@ -131,6 +133,14 @@ class OracleScene:
         orc.L.orc_scene_counts(h, c.ctypes.data)
         (self.W, self.H, self.n_vertices, self.n_tris, self.n_meshes, self.n_instances, self.n_lights,
          self.n_point, self.depth, self.n_mats) = [int(x) for x in c]
+
+    def set_atlas(self, rgba8):
+        """Build extension: (H, W, 4) uint8 atlas for the textured shading mode."""
+        self._atlas = np.ascontiguousarray(rgba8, np.uint8)
+        assert self.orc.L.orc_set_atlas(self.h, self._atlas.ctypes.data, self._atlas.shape[1], self._atlas.shape[0]) == 0
+
+    def set_textures(self, on=True):
+        assert self.orc.L.orc_set_textures(self.h, int(on)) == 0
 
     def __del__(self):
         try:

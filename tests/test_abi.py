@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == 1
+    assert rt.lib().rt_abi_version() == 2
 
 
 def test_library_is_gfx950_code(rt):

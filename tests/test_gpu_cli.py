@@ -93,3 +93,20 @@ def test_cpp_shim_scene_builder_frame(gpu, oracle, tmp_path):
     o = oracle.render(oracle.load(scene_path("world1"), 96, 72), spp=1, nthreads=8, want=("rgba",))
     assert np.array_equal(frame, o["rgba"])
     assert (frame != 0).any()
+
+
+def test_cli_textured_mode(oracle, tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_atlas
+    out = str(tmp_path / "t.ppm")
+    r = _run([CLI, "-c", scene_path("world8_tex"), "--width", "160", "--height", "120", "-b", "--textures",
+              "--out", out])
+    assert r.returncode == 0, r.stderr
+    o = oracle.load(scene_path("world8_tex"), 160, 120)
+    o.set_atlas(make_atlas.atlas())
+    o.set_textures(True)
+    rgba = oracle.render(o, spp=1, nthreads=8, want=("rgba",))["rgba"]
+    exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
+    got = _ppm_rgb(out)
+    assert np.abs(got.astype(int) - exp.astype(int)).max() <= 1 and (got != exp).mean() < 1e-3
