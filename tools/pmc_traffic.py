@@ -22,7 +22,7 @@ def is_timed_trace(name):
     if "trace_kernel<" not in name:
         return False
     mode = name.split("trace_kernel<", 1)[1].split(">", 1)[0].split(",")[-1].strip()
-    return mode in ("0", "1")
+    return mode.isdigit() and (int(mode) & 2) == 0          # MODE bit 1 = STATS
 
 
 def per_dispatch(root, counter, sel=is_timed_trace):
