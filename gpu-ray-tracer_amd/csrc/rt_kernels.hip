@@ -74,6 +74,8 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DMat* __restrict__ mats;
     const DLight* __restrict__ lights;
     const float4* node_pair;  // BVH child pairs, heap order (written by bvh_build_kernel), see BvhRefs
+    const float4* fnode;      // ordered LBVH of the fast kernel (bvh_build_kernel)
+    int n_real, ftree;        // its leaf count; 1 if usable (>= 2 leaves, depth <= 31)
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
@@ -132,6 +134,7 @@ __device__ __forceinline__ bool tri_accept(const DTri& T, const Ray& r, float be
 // (v_pk_*) slab arithmetic.  Pair 0 = (unused node 0, root).  Degenerate boxes are
 // stored as min=+inf, max=-inf.
 struct BvhRefs {
+    const float4* fnode;    // ordered LBVH records (fast kernel): [4 (n_real - 1)]
     const float4* pair;     // [3n]
     const int* leaf;        // [n]  instance of leaf node n+i (bvh.cu ordering[])
     const float4* inst;     // [n_inst] (px, py, pz, mesh | 0x80000000 if the pose is not identity)
@@ -155,9 +158,9 @@ __device__ __forceinline__ f2 vmax(f2 a, f2 b) { return f2{fmaxf(a.x, b.x), fmax
 // the RayInv bias (see ray_inv); rays with a non-finite reciprocal (ri.exact) and
 // boxes near a tie take the exact reference test.
 // tlo (pruning) is a lower bound of the exact entry distance, -inf if undecided.
-__device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
-                                         bool& h0, bool& h1, float& t0, float& t1) {
-    const float4 A = np[3 * k], B = np[3 * k + 1], C = np[3 * k + 2];
+__device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, const RayInv& ri, bool active,
+                                            bool& h0, bool& h1, float& t0, float& t1) {
+    const float4 A = rec[0], B = rec[1], C = rec[2];
     const bool nd0 = A.x <= B.z, nd1 = A.y <= B.w;            // nondegenerate (bounding_box.cu:63-65)
     t0 = -INFINITY; t1 = -INFINITY;
     auto exact = [&](int c) {
@@ -192,6 +195,10 @@ __device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, 
     h0 = active && nd0 && exact(0);
     h1 = active && nd1 && exact(1);
 #endif
+}
+__device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
+                                         bool& h0, bool& h1, float& t0, float& t1) {
+    pair_hit_at(np + 3 * k, r, ri, active, h0, h1, t0, t1);
 }
 
 struct Best { float time; int inst, tri; float u, v; };     // closest accepted triangle so far
@@ -336,11 +343,14 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 //    change Light::attenuate (light.cu:35-58).
 //  * triangle skip (cast_local's t_lo): a triangle whose plane crossing is certainly
 //    before tlo(leaf) - M cannot be accepted, so its inside test is not run.
-template <bool NOLEAF, bool STATS>
+template <bool NOLEAF, bool STATS, bool FT = false>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
-    const bool prune = !STATS && S.prune_abs >= 0.0f;
+#ifndef RT_NOPRUNE
+#define RT_NOPRUNE 0         // 1: profiling variant without distance pruning
+#endif
+    const bool prune = !RT_NOPRUNE && !STATS && S.prune_abs >= 0.0f;
     float im = 0.0f;                                           // max_a |1/d_a| (set below)
     auto slack = [&](float t) { return (S.prune_abs + 0x1p-14f * fabsf(t)) * im + 0x1p-14f * fabsf(t); };
     auto cut = [&]() {
@@ -366,6 +376,83 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     const int n = S.n_leaf;
     const RayInv ri = ray_inv(r);
     im = ri.exact ? INFINITY : fmaxf(fabsf(ri.ix), fmaxf(fabsf(ri.iy), fabsf(ri.iz)));
+    if (FT) {
+        // Ordered LBVH (fast kernel, S.ftree): same leaves and leaf order as the heap, so
+        // each lane meets exactly the leaves its ray hits, in the heap's DFS order (a
+        // hit leaf's ancestors contain it and are hit: the slab test is monotone in the
+        // box).  Wave-uniform stack of pending B children in lanes 0..31 of one VGPR
+        // (tree depth <= 31 is checked on the host): an internal node as its index, a
+        // leaf B as -2 - parent, whose pair test is re-run when it is popped (fresh hit
+        // and entry bound under the current cut).  Pruning and triangle skip as above.
+        DirPre pre{};
+        if (S.ident_all) pre = dir_pre(r.d);
+        const bool box_bound = S.prune_abs >= 0.0f;
+        auto t_low = [&](float tl) { return box_bound ? tl - slack(tl) : -INFINITY; };
+        auto leaf_i = [&](bool h, int ti, float tl) {
+            if (!__ballot(h)) return;
+            ti = uni(ti);
+            if (h && cast_local<false>(S, bv, ti, r, b, pre, wc, t_low(tl))) {
+                hit = true;
+                if (b.time <= occl_t) active = false;
+            }
+        };
+        int node = 0, sp = 0, stk = 0;
+        const int my_lane = __lane_id();
+        auto push = [&](int e) { stk = my_lane == sp ? e : stk; sp++; };   // v_writelane
+        for (;;) {
+            const float4* rec = bv.fnode + 4 * node;
+            bool h0, h1;
+            float t0, t1;
+            pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
+            const float4 rf = rec[3];
+            const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
+            if (prune) {
+                const float ct = cut();
+                h0 = h0 && !(t0 > ct);
+                h1 = h1 && !(t1 > ct);
+            }
+            bool goA = false, goB = false;
+            if (ra < 0) leaf_i(h0, -1 - ra, t0);
+            else goA = __ballot(h0) != 0;
+            if (rb < 0) {
+                const bool hb = h1 && !(prune && t1 > cut());
+                if (goA) {
+                    if (__ballot(hb)) push(-2 - node);
+                } else {
+                    leaf_i(hb, -1 - rb, t1);
+                }
+            } else {
+                goB = __ballot(h1) != 0;
+            }
+            if (!__ballot(active)) break;                      // every lane occluded
+            if (goA) {
+                if (goB) push(rb);
+                node = ra;
+                continue;
+            }
+            if (goB) { node = rb; continue; }
+            bool more = false;                                 // pop: pending leaves run, an internal node resumes
+            while (sp > 0) {
+                sp--;
+                const int e = __builtin_amdgcn_readlane(stk, sp);
+                if (e < 0) {                                   // leaf B of node -2 - e
+                    const float4* pr = bv.fnode + 4 * (-2 - e);
+                    bool g0, g1;
+                    float u0, u1;
+                    pair_hit_at(pr, r, ri, active, g0, g1, u0, u1);
+                    const int lb = uni(__float_as_int(pr[3].y));
+                    leaf_i(g1 && !(prune && u1 > cut()), -1 - lb, u1);
+                    if (!__ballot(active)) break;
+                    continue;
+                }
+                node = e;
+                more = true;
+                break;
+            }
+            if (!more) break;
+        }
+        return hit;
+    }
     if (STATS) wc.nodes += __popcll(am);                       // root test
     bool hr, hdummy;
     float tdummy, troot;
@@ -535,7 +622,7 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
 constexpr int PARK_FIELDS = 25;
-template <int NS, bool STATS, bool PARK, bool TEX>
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     Frame cur;
@@ -659,7 +746,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        const bool hit = closest_hit<false, STATS>(S, bv, need, q, b, wc, occl, lim);
+        const bool hit = closest_hit<false, STATS, FT>(S, bv, need, q, b, wc, occl, lim);
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -745,16 +832,26 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
 }
 
 // stage_bvh's LDS image size (16-B multiple)
-__host__ __device__ inline size_t lds_bytes(const SceneView& S) {
+__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false) {
+    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst;
     return ((48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + ((16 * (size_t)S.n_inst + 15) & ~(size_t)15);
 }
 
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
-template <bool LDS>
+template <bool LDS, bool FT = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
-    if (LDS) {
+    bv.fnode = S.fnode; bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    if (LDS && FT) {                                       // ordered LBVH | inst4
+        const int nf = 4 * (S.n_real - 1);
+        float4* fn = reinterpret_cast<float4*>(smem);
+        float4* in = fn + nf;
+        for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = S.fnode[i];
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        __syncthreads();
+        bv.fnode = fn; bv.inst = in;
+    } else if (LDS) {
         const int n3 = 3 * S.n_leaf;
         float4* np = reinterpret_cast<float4*>(smem);
         int* lf = reinterpret_cast<int*>(smem + 16 * (size_t)n3);
@@ -764,8 +861,6 @@ __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* 
         for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
         __syncthreads();
         bv.pair = np; bv.leaf = lf; bv.inst = in;
-    } else {
-        bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
     }
     return bv;
 }
@@ -786,17 +881,19 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 2 (PARK): park integrator state in LDS during queries (trace_sample); needs
 // PARK_FIELDS x 4 B x TRACE_BLOCK_P of LDS beside the BVH image.
 // MODE bit 3 (TEX): textured shading (hit_kd), generic frame depth only.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8;
+// MODE bit 4 (FT): traverse the ordered LBVH (closest_hit) instead of the reference heap.
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const BvhRefs bv = stage_bvh<LDS>(S, smem);
+    constexpr bool FT = (MODE & M_FT) != 0;
+    const BvhRefs bv = stage_bvh<LDS, FT>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool TEX = (MODE & M_TEX) != 0;
-    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S)) + threadIdx.x : nullptr;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
@@ -840,7 +937,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             }
             if (rd == 0) request(qi);                          // next ticket, in flight during the trace
             const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
             if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
@@ -929,8 +1026,43 @@ struct BvhArgs {
     Box* boxes;              // scratch: n instance boxes
     Box* tree;               // scratch: 2n-1 boxes, reference storage order
     float* node_pair;        // out: [12n] child-pair layout (BvhRefs); degenerate boxes: min=+inf, max=-inf
+    float4* fnode;           // out: ordered LBVH of the fast kernel, [4 (n_real-1)] (see FNode below)
+    int n_real;              // instances with a non-degenerate box (leaves of the ordered LBVH)
     int* leaf_inst;          // out: [n] instance of leaf node n+i
 };
+
+// Karras radix-tree node i over sorted 64-bit keys k[0, nr): range [first, last] and
+// split gamma (left = [first, gamma], right = [gamma+1, last]); equal keys are told
+// apart by their index (delta = 64 + clz(i ^ j)).
+__host__ __device__ inline int fnode_delta(const unsigned long long* k, int nr, int i, int j) {
+    if (j < 0 || j >= nr) return -1;
+    const unsigned long long x = k[i] ^ k[j];
+    if (x == 0) {
+        const unsigned y = (unsigned)(i ^ j);
+        return 64 + (y ? __builtin_clz(y) : 32);
+    }
+    return __builtin_clzll(x);
+}
+__host__ __device__ inline void fnode_split(const unsigned long long* k, int nr, int i, int& first, int& last, int& gamma) {
+    const int d = fnode_delta(k, nr, i, i + 1) - fnode_delta(k, nr, i, i - 1) >= 0 ? 1 : -1;
+    const int dmin = fnode_delta(k, nr, i, i - d);
+    int lmax = 2;
+    while (fnode_delta(k, nr, i, i + lmax * d) > dmin) lmax *= 2;
+    int l = 0;
+    for (int t = lmax / 2; t >= 1; t /= 2)
+        if (fnode_delta(k, nr, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = fnode_delta(k, nr, i, j);
+    int sp = 0;
+    for (int div = 2;; div *= 2) {
+        const int t = (l + div - 1) / div;
+        if (fnode_delta(k, nr, i, i + (sp + t) * d) > dnode) sp += t;
+        if (t <= 1) break;
+    }
+    gamma = i + sp * d + (d < 0 ? -1 : 0);
+    first = i < j ? i : j;
+    last = i < j ? j : i;
+}
 
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -993,6 +1125,25 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         float* q = A.node_pair + 12 * (k >> 1) + (k & 1);
         q[0] = b.mn.x; q[2] = b.mn.y; q[4] = b.mn.z; q[6] = b.mx.x; q[8] = b.mx.y; q[10] = b.mx.z;
         if (k >= n) A.leaf_inst[k - n] = idx[2 * n - 1 - k];
+    }
+    // Ordered LBVH (fast kernel): a radix tree (Karras 2012) over the same sorted
+    // leaves.  Internal node i splits at the highest differing key bit; the child
+    // whose leaves are later in storage order is child A (visited first), so
+    // leaves are met in the heap's DFS order (heap leaf k <-> storage 2n-1-k).
+    const int nr = A.n_real;                    // real leaves = storage [0, nr) (padding sorts last)
+    for (int i = tid; i < nr - 1; i += nt) {
+        int first, last, gamma;
+        fnode_split(keys, nr, i, first, last, gamma);
+        const int cl[2] = {gamma + 1, gamma}, lo[2] = {gamma + 1, first}, hi[2] = {last, gamma};
+        float* q = reinterpret_cast<float*>(A.fnode + 4 * (size_t)i);
+        int* refs = reinterpret_cast<int*>(A.fnode + 4 * (size_t)i + 3);
+        for (int c = 0; c < 2; c++) {                   // c = 0: child A (later leaves), 1: child B
+            Box b = A.tree[lo[c]];
+            for (int l = lo[c] + 1; l <= hi[c]; l++) b = merge(b, A.tree[l]);
+            q[0 + c] = b.mn.x; q[2 + c] = b.mn.y; q[4 + c] = b.mn.z; q[6 + c] = b.mx.x; q[8 + c] = b.mx.y; q[10 + c] = b.mx.z;
+            refs[c] = lo[c] == hi[c] ? -1 - idx[lo[c]] : cl[c];      // leaf: -1 - instance
+        }
+        refs[2] = refs[3] = 0;
     }
 }
 
@@ -1100,7 +1251,9 @@ struct rt_scene {
     // device buffers
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
     DLight* d_lights = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
-    float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_inst4 = nullptr;
+    float4* d_node_pair = nullptr; int* d_leaf = nullptr;
+    float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
+    float4* d_inst4 = nullptr;
     int* d_work = nullptr; int n_cu = 0;
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
@@ -1135,6 +1288,49 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
 }
 
 int upload_inst4(rt_scene* s);
+
+// Leaf count and depth (internal nodes on the longest root-leaf path) of the ordered
+// LBVH bvh_build_kernel will build: the same box, Morton and sort arithmetic on the
+// host (RT_HD functions).  The fast traversal's stack holds <= FT_MAX_DEPTH entries.
+constexpr int FT_MAX_DEPTH = 31;
+void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
+    std::vector<Box> mbox(h.d_meshes.size());
+    for (size_t m = 0; m < h.d_meshes.size(); m++) {
+        Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
+        const DMesh& mesh = h.d_meshes[m];
+        for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
+            fit_vertex(b, h.d_tris[t].a); fit_vertex(b, h.d_tris[t].b); fit_vertex(b, h.d_tris[t].c);
+        }
+        mbox[m] = from_local(b, mesh.pose);
+    }
+    std::vector<std::pair<unsigned long long, int>> kv;
+    for (size_t i = 0; i < h.d_insts.size(); i++) {
+        const Box b = from_local(mbox[h.d_insts[i].mesh], h.d_insts[i].pose);
+        if (b.nd) kv.push_back({z_order(neg(box_center(b))), (int)i});
+    }
+    std::stable_sort(kv.begin(), kv.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    const int nr = (int)kv.size();
+    *n_real = nr;
+    *depth = 0;
+    if (nr < 2) return;
+    std::vector<unsigned long long> keys(nr);
+    for (int i = 0; i < nr; i++) keys[i] = kv[i].first;
+    std::vector<int> child(2 * (nr - 1));                   // internal children (-1: leaf)
+    for (int i = 0; i < nr - 1; i++) {
+        int first, last, gamma;
+        fnode_split(keys.data(), nr, i, first, last, gamma);
+        child[2 * i] = gamma + 1 == last ? -1 : gamma + 1;
+        child[2 * i + 1] = gamma == first ? -1 : gamma;
+    }
+    std::vector<std::pair<int, int>> todo{{0, 1}};
+    while (!todo.empty()) {
+        const auto [node, d] = todo.back();
+        todo.pop_back();
+        *depth = std::max(*depth, d);
+        if (d > nr) { *depth = 1 << 20; return; }          // malformed: disable the fast tree
+        for (int c = 0; c < 2; c++) if (child[2 * node + c] >= 0) todo.push_back({child[2 * node + c], d + 1});
+    }
+}
 void free_atlas(rt_scene* s);
 int ensure_atlas(rt_scene* s);
 
@@ -1167,6 +1363,8 @@ int upload(rt_scene* s) {
     s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
     HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
+    ordered_tree_shape(h, &s->n_real, &s->fdepth);
+    HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_work, 16 * NQ * sizeof(int)));
@@ -1237,6 +1435,7 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.tris = s->d_tris; A.n = s->n_leaf;
     A.boxes = s->d_boxes; A.tree = s->d_tree;
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
+    A.fnode = s->d_fnode; A.n_real = s->n_real;
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
@@ -1249,7 +1448,12 @@ int build_bvh(rt_scene* s, hipStream_t st) {
 SceneView view_of(const rt_scene* s, bool use_bvh) {
     SceneView v;
     v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
-    v.node_pair = s->d_node_pair; v.leaf_inst = s->d_leaf; v.inst4 = s->d_inst4;
+    v.node_pair = s->d_node_pair; v.leaf_inst = s->d_leaf;
+    v.fnode = s->d_fnode; v.n_real = s->n_real;
+#ifndef RT_NO_FTREE
+#define RT_NO_FTREE 0        // 1: profiling variant, the fast kernel walks the reference heap
+#endif
+    v.ftree = (!RT_NO_FTREE && s->n_real >= 2 && s->fdepth <= FT_MAX_DEPTH) ? 1 : 0; v.inst4 = s->d_inst4;
     v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
     v.ident_all = 1;
@@ -1305,7 +1509,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
-    const size_t lds = lds_bytes(S);
+    const bool tex = o.textures != 0;
+    const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
+    const bool ft = !tex && mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
+    const size_t lds = lds_bytes(S, ft);
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
     const void* fn;
@@ -1321,11 +1528,16 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, false, 10>, (const void*)trace_kernel<NG, false, 11>},
         {(const void*)trace_kernel<NG, true, 8>, (const void*)trace_kernel<NG, true, 9>,
          (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
-    const bool tex = o.textures != 0;
     const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
     if (tex) {
         fn = textured[use_lds ? 1 : 0][mode];
+    } else if (ft) {
+        constexpr int PF = M_PARK | M_FT;
+        fn = park ? (ns <= 0 ? (const void*)trace_kernel<0, true, PF> : ns <= 2 ? (const void*)trace_kernel<2, true, PF>
+                                                                         : (const void*)trace_kernel<NG, true, PF>)
+                  : (ns <= 0 ? (const void*)trace_kernel<0, true, M_FT> : ns <= 2 ? (const void*)trace_kernel<2, true, M_FT>
+                                                                           : (const void*)trace_kernel<NG, true, M_FT>);
     } else if (park) {
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, M_PARK> : ns <= 2 ? (const void*)trace_kernel<2, true, M_PARK>
                      : (const void*)trace_kernel<NG, true, M_PARK>;
@@ -1364,6 +1576,7 @@ void invalidate(rt_scene* s) { s->bvh_valid = false; }
 rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
     free_atlas(this);
+    dfree(d_fnode);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
