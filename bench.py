@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-rows", type=int, default=1, help="CPU baseline renders rows y %% k == 0")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
+                        "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
     return p.parse_args()
 
 
@@ -91,19 +94,24 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = max(world, 1)
-    torch.cuda.set_device(local)
+    dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     dist = None
+    gloo = world > 1 and args.dist_backend == "gloo"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    rtamd.set_device(local)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    rtamd.set_device(dev)
     scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")
     scene = rtamd.Scene.load_json(scene_path, args.width, args.height)
     if args.textures:
         scene.load_atlas()
     W, H = scene.width, scene.height
     my_rows = len(rtdist.rows_of(rank, world, H))
-    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist)
+    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo)
     part = fb.part
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
@@ -143,8 +151,9 @@ def main():
     torch.cuda.synchronize()
     rb_ms = (time.perf_counter() - t2) / max(1, args.steps // 2) * 1e3
 
-    local_rays = torch.tensor([st["rays"], st["nodes"], st["leaves"], st["tri_tests"]], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    red_dev = "cpu" if gloo else "cuda"
+    local_rays = torch.tensor([st["rays"], st["nodes"], st["leaves"], st["tri_tests"]], dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if dist:
         dist.all_reduce(local_rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -178,7 +187,8 @@ def main():
         "config": {"workload": "%s.json %dx%d %dspp %s%s" % (args.scene, W, H, args.spp, "brute" if args.brute else "BVH",
                                                           " textured" if args.textures else ""),
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bvh": use_bvh,
-                   "parallelism": "row-cyclic x%d + RCCL gather" % world if world > 1 else "single GPU"},
+                   "parallelism": ("row-cyclic x%d + %s gather" % (world, "gloo host-staged" if gloo else "RCCL"))
+                                  if world > 1 else "single GPU"},
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
         "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),
         "tri_tests_per_frame": int(tris), "trace_kernel_ms": round(trace_ms, 4), "bvh_build_ms": round(bvh_ms, 4),

@@ -28,22 +28,26 @@ class RowCyclicFrame:
     row_step = world, compact = 1); `gather()` assembles the frame on rank 0.
     """
 
-    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32):
+    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, host_staging=False):
+        """host_staging: gather through host memory (backends without device tensors,
+        e.g. gloo when testing the multi-rank path on one GPU)."""
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
+        self.host_staging = host_staging
         self.rows = slice_height(world, height)
         self.part = torch.zeros((self.rows, width), dtype=dtype, device=device)
-        self.gathered = ([torch.empty_like(self.part) for _ in range(world)]
+        gdev = "cpu" if host_staging else device
+        self.gathered = ([torch.empty((self.rows, width), dtype=dtype, device=gdev) for _ in range(world)]
                          if (world > 1 and rank == 0) else None)
         self.frame = torch.empty((height, width), dtype=dtype, device=device) if rank == 0 else None
 
     def gather(self):
         """Collect every rank's slice on rank 0 and un-permute the rows into `frame`."""
         if self.world > 1:
-            self.dist.gather(self.part, self.gathered, dst=0)
+            self.dist.gather(self.part.cpu() if self.host_staging else self.part, self.gathered, dst=0)
             if self.rank == 0:
                 for r in range(self.world):
                     n = len(rows_of(r, self.world, self.H))
-                    self.frame[r::self.world] = self.gathered[r][:n]
+                    self.frame[r::self.world] = self.gathered[r][:n].to(self.frame.device)
         elif self.rank == 0:
             self.frame.copy_(self.part[:self.H])
         return self.frame
