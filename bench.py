@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-rows", type=int, default=1, help="CPU baseline renders rows y %% k == 0")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--no-kernel-timing", action="store_true",
+                   help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -134,7 +136,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(not args.no_kernel_timing)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -168,6 +170,8 @@ def main():
     value = rays * args.steps / elapsed / 1e6
     # roofline of the dominant kernel (trace), this rank: algorithmic bytes per launch / event-timed duration
     trace_ms = tm["trace_ms_total"] / max(1, tm["frames"])
+    if tm["frames"] == 0:                                   # --no-kernel-timing: fall back to the step time
+        trace_ms = ms_per_step
     bvh_ms = tm["bvh_ms_total"] / max(1, tm["frames"])
     algo_bytes = B_NODE * st["nodes"] + B_LEAF * st["leaves"] + 4 * W * my_rows
     achieved = algo_bytes / (trace_ms * 1e-3) / 1e9

@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <numeric>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -55,7 +56,10 @@ constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LD
 constexpr int TRACE_BLOCK_P = RT_BLOCK;  // persistent block: 12 waves (3 per SIMD, 168-VGPR budget) sharing one LDS BVH copy
 constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
 constexpr int PARK_LDS_LIMIT = 158 * 1024;   // BVH image + parking area (160 KB per CU)
-constexpr int NQ = 8;                    // work queues (one per XCD dispatch slot), 64-B apart
+#ifndef RT_NQ
+#define RT_NQ 8
+#endif
+constexpr int NQ = RT_NQ;                    // work queues (one per XCD dispatch slot), 64-B apart
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -554,6 +558,7 @@ struct TraceParams {
     V4 ambience;
     int W, H, row0, row_step, n_rows, compact, spp, depth;
     int lanes_per_px, px_per_wave, gw, gh, n_gx, n_groups;   // sample-parallel lane mapping
+    int scramble;             // ticket -> group permutation factor (coprime with the queue length)
     const float2* __restrict__ spp_off;
     uint32_t* rgba;
     float4* radiance;
@@ -915,10 +920,15 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     request(0);
     int ticket = resolve();
     const unsigned long long c_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rt_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;   // global 100 MHz clock
     for (;;) {
         while (qi < NQ && ticket >= per_q) { qi++; if (qi < NQ) { request(qi); ticket = resolve(); } }
         if (qi >= NQ) break;
-        const int g = ((q0 + qi) % NQ) + NQ * ticket;
+        // tickets visit the queue's groups in a scrambled order (t * scramble mod per_q, a
+        // bijection): expensive image regions are spread over the frame instead of all
+        // starting last and leaving a long tail of idle CUs (measured: first wave done at
+        // 69% of the kernel span with row order)
+        const int g = ((q0 + qi) % NQ) + NQ * (int)(((long long)ticket * P.scramble) % per_q);
         if (g >= P.n_groups) { request(qi); ticket = resolve(); continue; }
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
@@ -973,6 +983,12 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         atomicAdd(&P.stats[10], __builtin_amdgcn_s_memtime() - c_start);
         atomicAdd(&P.stats[11], wc.cyc_sample); atomicAdd(&P.stats[12], wc.cyc_post);
         atomicAdd(&P.stats[13], wc.wbary); atomicAdd(&P.stats[14], wc.lbary);
+        const unsigned long long rt_end = __builtin_amdgcn_s_memrealtime();
+        atomicMin(&P.stats[15], rt_start);                      // kernel span (earliest start, latest end)
+        atomicMax(&P.stats[16], rt_end);
+        atomicAdd(&P.stats[17], rt_end - rt_start);             // summed wave lifetimes (same clock)
+        atomicMax(&P.stats[18], rt_start);                      // latest start / earliest end
+        atomicMin(&P.stats[19], rt_end);
     }
 }
 
@@ -1019,6 +1035,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams
 // in one workgroup.  Output: heap-ordered nodes[1 .. 2n-1].
 // ---------------------------------------------------------------------------
 struct BvhArgs {
+    int* work; int n_work;   // the trace kernel's work counters, zeroed here (saves a memset launch)
     const DInst* insts; int n_inst;
     const DMesh* meshes; int n_meshes;
     const DTri* tris;
@@ -1071,6 +1088,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     Box* mbox = reinterpret_cast<Box*>(smem + 12 * (size_t)A.n);
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n = A.n;
+    for (int i = tid; i < A.n_work; i += nt) A.work[i] = 0;
 
     // mesh boxes: Trimesh::compute_bounding_box (trimesh.cu:21-32), sequential fit order
     for (int m = tid; m < A.n_meshes; m += nt) {
@@ -1255,6 +1273,7 @@ struct rt_scene {
     float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
     float4* d_inst4 = nullptr;
     int* d_work = nullptr; int n_cu = 0;
+    bool work_zeroed = false;                    // bvh_build_kernel zeroed d_work for the next trace launch
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
     uint32_t* d_canvas = nullptr;
@@ -1371,7 +1390,7 @@ int upload(rt_scene* s) {
     if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
-    HIPCHK(hipMalloc((void**)&s->d_stats, 16 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&s->d_stats, 24 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
@@ -1415,6 +1434,15 @@ int ensure_atlas(rt_scene* s) {
     return RT_OK;
 }
 
+// A factor coprime with the queue length, so t -> t * f mod len is a permutation
+// (checked with gcd; f near len * 0.618 spreads consecutive tickets across the image).
+int ticket_scramble(int len) {
+    if (len <= 2) return 1;
+    int f = (int)(len * 0.6180339887) | 1;
+    while (std::gcd(f % len, len) != 1) f++;
+    return f % len;
+}
+
 int ensure_spp(rt_scene* s, int spp) {
     if (spp <= s->spp_cap) return RT_OK;
     int cap = std::max(spp, 64);
@@ -1436,12 +1464,14 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.boxes = s->d_boxes; A.tree = s->d_tree;
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     A.fnode = s->d_fnode; A.n_real = s->n_real;
+    A.work = s->d_work; A.n_work = 16 * NQ;
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
     hipLaunchKernelGGL(bvh_build_kernel, dim3(1), dim3(1024), lds, st, A);
     HIPCHK(hipGetLastError());
     s->bvh_valid = true;
+    s->work_zeroed = true;
     return RT_OK;
 }
 
@@ -1506,9 +1536,11 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.gw = gw; P.gh = P.px_per_wave / gw;
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
+    P.scramble = ticket_scramble((P.n_groups + NQ - 1) / NQ);
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
-    HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
+    if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
+    s->work_zeroed = false;                                   // this launch consumes the counters
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     const bool ft = !tex && mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
@@ -1899,7 +1931,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         s->tev_used += 3;
         HIPCHK(hipEventRecord(te[0], st));
     }
-    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
+    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st)) != RT_OK) return r;
     }
@@ -2028,7 +2060,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
-            HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), s->stream));
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), s->stream));
+            HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), s->stream));
+            HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), s->stream));
             HIPCHK(hipEventRecord(s->ev[0], s->stream));
             if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0)) != RT_OK) return r;
             HIPCHK(hipEventRecord(s->ev[1], s->stream));
@@ -2036,9 +2070,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
-        unsigned long long v[15];
+        unsigned long long v[20];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-        if (counters) for (int i = 0; i < 15; i++) counters[i] = v[i];
+        if (counters) for (int i = 0; i < 20; i++) counters[i] = v[i];
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
@@ -2046,6 +2080,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, spp)) != RT_OK) return r;
     if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+    s->work_zeroed = false;                                  // the primary kernels reset d_work themselves
     rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
     TraceParams P{};
     const rt::Scene& h = s->h;
@@ -2070,7 +2105,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     float total = 0;
     for (int i = 0; i < reps; i++) {
         HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), s->stream));
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 16 * sizeof(unsigned long long), s->stream));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), s->stream));
         HIPCHK(hipEventRecord(s->ev[0], s->stream));
         void* args[] = {&P, &S, &out};
         HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, s->stream));
@@ -2079,9 +2114,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
-    unsigned long long v[15];
+    unsigned long long v[20];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 15; i++) counters[i] = v[i];
+    if (counters) for (int i = 0; i < 20; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;

@@ -38,7 +38,9 @@ class RowCyclicFrame:
         gdev = "cpu" if host_staging else device
         self.gathered = ([torch.empty((self.rows, width), dtype=dtype, device=gdev) for _ in range(world)]
                          if (world > 1 and rank == 0) else None)
-        self.frame = torch.empty((height, width), dtype=dtype, device=device) if rank == 0 else None
+        # one rank: the slice is the frame (rows_of(0, 1, H) = every row, in order) -- no copy
+        self.frame = (self.part if world == 1 else
+                      torch.empty((height, width), dtype=dtype, device=device) if rank == 0 else None)
 
     def gather(self):
         """Collect every rank's slice on rank 0 and un-permute the rows into `frame`."""
@@ -48,6 +50,4 @@ class RowCyclicFrame:
                 for r in range(self.world):
                     n = len(rows_of(r, self.world, self.H))
                     self.frame[r::self.world] = self.gathered[r][:n].to(self.frame.device)
-        elif self.rank == 0:
-            self.frame.copy_(self.part[:self.H])
         return self.frame
