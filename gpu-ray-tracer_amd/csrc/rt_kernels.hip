@@ -565,7 +565,15 @@ struct TraceParams {
     int* hit_inst;
     int* hit_tri;
     unsigned long long* stats;
-    int* work;                // persistent-wave work counter (zeroed before each launch)
+    int* work;                // persistent-wave work counters (zeroed before each launch); work[16 NQ]: heavy list
+    // Longest-first scheduling history (fast frames only, hist = 1): the previous frame's
+    // heavy groups (hl_prev[0, *hc_prev)) run first and are skipped in the normal queues
+    // (hf_prev); this frame records its own into the *_next buffers.  hs_* = summed group
+    // durations (100 MHz ticks) for the threshold (4x the mean group).
+    int hist;
+    const int* hl_prev; int* hl_next;
+    const unsigned char* hf_prev; unsigned char* hf_next;
+    const unsigned long long* hctl_prev; unsigned long long* hctl_next;   // {count, sum}
     int occl_exit;            // shadow-ray occlusion early exit (all-opaque scene, no statistics)
     const float4* atlas;      // textured mode: atlas texels, byte / 255 (rt_scene_set_atlas)
     int atlas_w, atlas_h;
@@ -908,28 +916,36 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     // measured) and a static split left a 1.5x load-imbalance tail (measured).
     const int q0 = blockIdx.x % NQ;
     const int per_q = (P.n_groups + NQ - 1) / NQ;
-    int qi = 0;
+    int n_heavy = 0;
+    unsigned long long thr = ~0ull, wave_sum = 0;
+    if (P.hist) {
+        n_heavy = (int)P.hctl_prev[0];
+        if (P.hctl_prev[1]) thr = 4 * P.hctl_prev[1] / (unsigned long long)P.n_groups;
+    }
+    int qi = n_heavy > 0 ? -1 : 0;                           // -1: the previous frame's heavy groups first
     // Lane 0 holds the raw result of the pending ticket request.  It is requested after
     // the group's own global loads (vmcnt retires in order, so an earlier atomic would
     // hold them up) and read only when the next group starts.
     int pend = 0;
     auto request = [&](int q) {
-        if (lane == 0) pend = atomicAdd(&P.work[16 * ((q0 + q) % NQ)], 1);
+        if (lane == 0) pend = atomicAdd(q < 0 ? &P.work[16 * NQ] : &P.work[16 * ((q0 + q) % NQ)], 1);
     };
     auto resolve = [&]() { return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
-    request(0);
+    request(qi);
     int ticket = resolve();
     const unsigned long long c_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long rt_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;   // global 100 MHz clock
     for (;;) {
-        while (qi < NQ && ticket >= per_q) { qi++; if (qi < NQ) { request(qi); ticket = resolve(); } }
+        while (qi < NQ && ticket >= (qi < 0 ? n_heavy : per_q)) { qi++; if (qi < NQ) { request(qi); ticket = resolve(); } }
         if (qi >= NQ) break;
         // tickets visit the queue's groups in a scrambled order (t * scramble mod per_q, a
         // bijection): expensive image regions are spread over the frame instead of all
         // starting last and leaving a long tail of idle CUs (measured: first wave done at
         // 69% of the kernel span with row order)
-        const int g = ((q0 + qi) % NQ) + NQ * (int)(((long long)ticket * P.scramble) % per_q);
-        if (g >= P.n_groups) { request(qi); ticket = resolve(); continue; }
+        const int g = qi < 0 ? uni(P.hl_prev[ticket])
+                             : ((q0 + qi) % NQ) + NQ * (int)(((long long)ticket * P.scramble) % per_q);
+        if (g >= P.n_groups || (qi >= 0 && P.hist && P.hf_prev[g])) { request(qi); ticket = resolve(); continue; }
+        const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
         const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
@@ -937,6 +953,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
         const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
+        const unsigned long long g_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         for (int rd = 0; rd < rounds; rd++) {
             const int k = rd * L + sub;
             const bool act = valid && k < P.spp;
@@ -970,8 +987,20 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
+        if (STATS && P.stats && lane == 0) {                  // profiling: heaviest group
+            atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
+            atomicMax(&P.stats[21], wc.wq - g_q0);
+        }
+        if (P.hist && lane == 0) {                            // record for the next frame's order
+            const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;
+            const bool heavy = dur > thr;
+            P.hf_next[g] = heavy ? 1 : 0;
+            if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
+            wave_sum += dur;
+        }
         ticket = resolve();
     }
+    if (P.hist && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
     if (STATS && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
         if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
@@ -1274,6 +1303,12 @@ struct rt_scene {
     float4* d_inst4 = nullptr;
     int* d_work = nullptr; int n_cu = 0;
     bool work_zeroed = false;                    // bvh_build_kernel zeroed d_work for the next trace launch
+    // longest-first scheduling history (TraceParams::hist): double-buffered by frame parity
+    int* d_hlist[2] = {nullptr, nullptr};
+    unsigned char* d_hflag[2] = {nullptr, nullptr};
+    unsigned long long* d_hctl = nullptr;        // [2][count, sum]
+    int hist_cap = 0, hist_parity = 0;
+    long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
     uint32_t* d_canvas = nullptr;
@@ -1386,7 +1421,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&s->d_work, 16 * NQ * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&s->d_work, 16 * (NQ + 1) * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
@@ -1443,6 +1478,29 @@ int ticket_scramble(int len) {
     return f % len;
 }
 
+// (Re)allocate / reset the scheduling history when the launch layout changes.
+int ensure_history(rt_scene* s, int n_groups, const long long* key, hipStream_t st) {
+    if (n_groups > s->hist_cap) {
+        for (int p = 0; p < 2; p++) { dfree(s->d_hlist[p]); dfree(s->d_hflag[p]); }
+        dfree(s->d_hctl);
+        const int cap = std::max(n_groups, 1024);
+        for (int p = 0; p < 2; p++) {
+            HIPCHK(hipMalloc((void**)&s->d_hlist[p], cap * sizeof(int)));
+            HIPCHK(hipMalloc((void**)&s->d_hflag[p], cap));
+        }
+        HIPCHK(hipMalloc((void**)&s->d_hctl, 4 * sizeof(unsigned long long)));
+        s->hist_cap = cap;
+        s->hist_key[0] = -1;
+    }
+    if (memcmp(key, s->hist_key, sizeof s->hist_key) != 0) {
+        for (int p = 0; p < 2; p++) HIPCHK(hipMemsetAsync(s->d_hflag[p], 0, s->hist_cap, st));
+        HIPCHK(hipMemsetAsync(s->d_hctl, 0, 4 * sizeof(unsigned long long), st));
+        memcpy(s->hist_key, key, sizeof s->hist_key);
+        s->hist_parity = 0;
+    }
+    return RT_OK;
+}
+
 int ensure_spp(rt_scene* s, int spp) {
     if (spp <= s->spp_cap) return RT_OK;
     int cap = std::max(spp, 64);
@@ -1464,7 +1522,7 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.boxes = s->d_boxes; A.tree = s->d_tree;
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     A.fnode = s->d_fnode; A.n_real = s->n_real;
-    A.work = s->d_work; A.n_work = 16 * NQ;
+    A.work = s->d_work; A.n_work = 16 * (NQ + 1);
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
@@ -1539,7 +1597,21 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.scramble = ticket_scramble((P.n_groups + NQ - 1) / NQ);
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
-    if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * NQ * sizeof(int), st));
+    if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * (NQ + 1) * sizeof(int), st));
+    // longest-first history (fast frames): valid while the launch layout is unchanged
+    P.hist = 0;
+    if (!want_stats && !dbg) {
+        const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
+        int r;
+        if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
+        const int prev = s->hist_parity, next = 1 - prev;
+        P.hist = 1;
+        P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
+        P.hf_prev = s->d_hflag[prev]; P.hf_next = s->d_hflag[next];
+        P.hctl_prev = s->d_hctl + 2 * prev; P.hctl_next = s->d_hctl + 2 * next;
+        HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
+        s->hist_parity = next;
+    }
     s->work_zeroed = false;                                   // this launch consumes the counters
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
@@ -1609,6 +1681,8 @@ rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
     free_atlas(this);
     dfree(d_fnode);
+    for (int p = 0; p < 2; p++) { dfree(d_hlist[p]); dfree(d_hflag[p]); }
+    dfree(d_hctl);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
@@ -2070,9 +2144,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
-        unsigned long long v[20];
+        unsigned long long v[22];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-        if (counters) for (int i = 0; i < 20; i++) counters[i] = v[i];
+        if (counters) for (int i = 0; i < 22; i++) counters[i] = v[i];
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
@@ -2114,9 +2188,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
-    unsigned long long v[20];
+    unsigned long long v[22];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 20; i++) counters[i] = v[i];
+    if (counters) for (int i = 0; i < 22; i++) counters[i] = v[i];
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;

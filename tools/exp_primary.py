@@ -11,7 +11,7 @@ L.rt_experiment.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.
 scene = sys.argv[1] if len(sys.argv) > 1 else "world8_stress"
 for which, spp in [(int(w), 8) for w in (sys.argv[2].split(',') if len(sys.argv) > 2 else ['3', '2', '4'])]:
     s = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", scene + ".json"), 1920, 1080)
-    ms = ctypes.c_double(); c = (ctypes.c_uint64 * 20)()
+    ms = ctypes.c_double(); c = (ctypes.c_uint64 * 22)()
     rtamd._check(L.rt_experiment(s._h, which, spp, 6, ctypes.byref(ms), c))
     print(json.dumps({"scene": scene, "which": which, "lib": os.path.basename(rtamd.LIB_PATH), "spp": spp, "ms": ms.value, "rays": c[0], "nodes": c[1], "leaves": c[2],
                       "Mrays_s": c[0] / ms.value / 1e3,
@@ -23,4 +23,5 @@ for which, spp in [(int(w), 8) for w in (sys.argv[2].split(',') if len(sys.argv)
                       "wave_inside_tests": c[13], "lane_inside_tests": c[14],
                       "wave_busy_over_span": c[17] / max(1, (c[16] - c[15]) * 3072),
                       "span_ms": (c[16] - c[15]) / 1e5, "latest_start_ms": (c[18] - c[15]) / 1e5,
-                      "earliest_end_ms": (c[19] - c[15]) / 1e5}))
+                      "earliest_end_ms": (c[19] - c[15]) / 1e5, "max_group_ms": c[20] / 1e5,
+                      "max_group_wave_queries": c[21]}))
