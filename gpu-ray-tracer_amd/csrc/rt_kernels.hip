@@ -20,6 +20,7 @@
 //    with scalar loads, `__ballot` decides descend vs. skip (scene.cu:54-70).
 //    Leaf and box tests use the reference's exact float32 operations, so hit
 //    indices are bit-identical to the single-ray semantics.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1065,6 +1066,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams
 // ---------------------------------------------------------------------------
 struct BvhArgs {
     int* work; int n_work;   // the trace kernel's work counters, zeroed here (saves a memset launch)
+    unsigned long long* hctl; // next frame's heavy-list counters (2 words), zeroed here too (may be null)
     const DInst* insts; int n_inst;
     const DMesh* meshes; int n_meshes;
     const DTri* tris;
@@ -1118,6 +1120,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n = A.n;
     for (int i = tid; i < A.n_work; i += nt) A.work[i] = 0;
+    if (A.hctl && tid < 2) A.hctl[tid] = 0;
 
     // mesh boxes: Trimesh::compute_bounding_box (trimesh.cu:21-32), sequential fit order
     for (int m = tid; m < A.n_meshes; m += nt) {
@@ -1185,8 +1188,15 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         float* q = reinterpret_cast<float*>(A.fnode + 4 * (size_t)i);
         int* refs = reinterpret_cast<int*>(A.fnode + 4 * (size_t)i + 3);
         for (int c = 0; c < 2; c++) {                   // c = 0: child A (later leaves), 1: child B
-            Box b = A.tree[lo[c]];
-            for (int l = lo[c] + 1; l <= hi[c]; l++) b = merge(b, A.tree[l]);
+            // box of storage leaves [lo, hi]: the level arrays of A.tree are a segment
+            // tree over storage order, so O(2 log n) aligned blocks cover the range
+            // (min/max merges are exact, any grouping gives the same bounds)
+            Box b;
+            b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
+            for (int l = lo[c], r = hi[c] + 1, off = 0, size = n; l < r; l >>= 1, r >>= 1, off += size, size >>= 1) {
+                if (l & 1) b = merge(b, A.tree[off + l++]);
+                if (r & 1) b = merge(b, A.tree[off + --r]);
+            }
             q[0 + c] = b.mn.x; q[2 + c] = b.mn.y; q[4 + c] = b.mn.z; q[6 + c] = b.mx.x; q[8 + c] = b.mx.y; q[10 + c] = b.mx.z;
             refs[c] = lo[c] == hi[c] ? -1 - idx[lo[c]] : cl[c];      // leaf: -1 - instance
         }
@@ -1308,6 +1318,7 @@ struct rt_scene {
     unsigned char* d_hflag[2] = {nullptr, nullptr};
     unsigned long long* d_hctl = nullptr;        // [2][count, sum]
     int hist_cap = 0, hist_parity = 0;
+    int hctl_zeroed = -1;                        // heavy-list slot the pending bvh_build_kernel zeroes (-1: none)
     long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
@@ -1316,7 +1327,7 @@ struct rt_scene {
     float4* d_atlas = nullptr;                   // atlas texels (float4, byte / 255)
     bool atlas_dirty = false;
     void* d_out[4] = {nullptr, nullptr, nullptr, nullptr};   // staging for host_outputs
-    std::vector<hipEvent_t> tev;      // timing=1 event triples (pool)
+    std::vector<hipEvent_t> tev;      // timing=1 events, 4 per frame: bvh start/stop, trace start/stop (pool)
     size_t tev_used = 0;
     size_t d_out_px = 0;
     int n_leaf = 0;
@@ -1513,8 +1524,12 @@ int ensure_spp(rt_scene* s, int spp) {
     return RT_OK;
 }
 
-int build_bvh(rt_scene* s, hipStream_t st) {
-    if (s->n_leaf == 0) { s->bvh_valid = true; return RT_OK; }
+int build_bvh(rt_scene* s, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+    if (s->n_leaf == 0) {
+        if (e0) { HIPCHK(hipEventRecord(e0, st)); HIPCHK(hipEventRecord(e1, st)); }
+        s->bvh_valid = true;
+        return RT_OK;
+    }
     BvhArgs A;
     A.insts = s->d_insts; A.n_inst = (int)s->h.d_insts.size();
     A.meshes = s->d_meshes; A.n_meshes = (int)s->h.d_meshes.size();
@@ -1523,10 +1538,15 @@ int build_bvh(rt_scene* s, hipStream_t st) {
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     A.fnode = s->d_fnode; A.n_real = s->n_real;
     A.work = s->d_work; A.n_work = 16 * (NQ + 1);
+    // the slot the next fast frame records its heavy list into (launch_trace skips its memset)
+    A.hctl = s->d_hctl ? s->d_hctl + 2 * (1 - s->hist_parity) : nullptr;
+    s->hctl_zeroed = s->d_hctl ? 1 - s->hist_parity : -1;
     size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
     lds = (lds + 15) & ~size_t(15);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
-    hipLaunchKernelGGL(bvh_build_kernel, dim3(1), dim3(1024), lds, st, A);
+    void* args[] = {&A};
+    // e0/e1 (timing=1): timestamps taken by the dispatch itself, no marker packets
+    HIPCHK(hipExtLaunchKernel((const void*)bvh_build_kernel, dim3(1), dim3(1024), args, lds, st, e0, e1, 0));
     HIPCHK(hipGetLastError());
     s->bvh_valid = true;
     s->work_zeroed = true;
@@ -1568,13 +1588,16 @@ bool opaque_scene(const rt_scene* s) {
 }
 
 int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y,
-                 bool want_stats, int occl_force = -1) {
+                 bool want_stats, int occl_force = -1, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     TraceParams P{};
     const rt::Scene& h = s->h;
     P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
     P.W = h.cam.W; P.H = h.cam.H; P.row0 = o.row0; P.row_step = o.row_step;
     P.n_rows = (P.H - o.row0 + o.row_step - 1) / o.row_step;
-    if (P.n_rows <= 0) return RT_OK;
+    if (P.n_rows <= 0) {
+        if (e0) { HIPCHK(hipEventRecord(e0, st)); HIPCHK(hipEventRecord(e1, st)); }
+        return RT_OK;
+    }
     P.compact = o.compact; P.spp = o.spp; P.depth = h.depth;
     P.spp_off = s->d_spp;
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
@@ -1609,10 +1632,11 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
         P.hf_prev = s->d_hflag[prev]; P.hf_next = s->d_hflag[next];
         P.hctl_prev = s->d_hctl + 2 * prev; P.hctl_next = s->d_hctl + 2 * next;
-        HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
+        if (s->hctl_zeroed != next) HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
         s->hist_parity = next;
     }
     s->work_zeroed = false;                                   // this launch consumes the counters
+    s->hctl_zeroed = -1;
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     const bool ft = !tex && mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
@@ -1656,7 +1680,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
     void* args[] = {&P, &S};
-    HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st));
+    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, e0, e1, 0));
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
@@ -1997,20 +2021,23 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     const bool timed = stats != nullptr;
     hipEvent_t* te = nullptr;
     if (o->timing) {
-        if (s->tev_used + 3 > s->tev.size()) {
-            if (s->tev.size() >= 3 * 4096) return fail(RT_ERR_STATE, "too many timed frames pending: call rt_timing_collect");
-            for (int i = 0; i < 3 * 64; i++) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); s->tev.push_back(e); }
+        if (s->tev_used + 4 > s->tev.size()) {
+            if (s->tev.size() >= 4 * 4096) return fail(RT_ERR_STATE, "too many timed frames pending: call rt_timing_collect");
+            for (int i = 0; i < 4 * 64; i++) { hipEvent_t e; HIPCHK(hipEventCreate(&e)); s->tev.push_back(e); }
         }
         te = &s->tev[s->tev_used];
-        s->tev_used += 3;
-        HIPCHK(hipEventRecord(te[0], st));
+        s->tev_used += 4;
     }
     if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
-        if ((r = build_bvh(s, st)) != RT_OK) return r;
+        if ((r = build_bvh(s, st, te ? te[0] : nullptr, te ? te[1] : nullptr)) != RT_OK) {
+            if (te) s->tev_used -= 4;                            // the frame's events stay unrecorded
+            return r;
+        }
+    } else if (te) {
+        HIPCHK(hipEventRecord(te[0], st)); HIPCHK(hipEventRecord(te[1], st));
     }
     if (timed) HIPCHK(hipEventRecord(s->ev[1], st));
-    if (te) HIPCHK(hipEventRecord(te[1], st));
     rt_render_opts oo = *o;
     const size_t W = s->h.cam.W, H = s->h.cam.H;
     const size_t n_rows = (H > (size_t)o->row0) ? (H - o->row0 + o->row_step - 1) / o->row_step : 0;
@@ -2028,9 +2055,11 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         oo.hit_tri = o->hit_tri ? (int32_t*)s->d_out[3] : nullptr;
     }
     uint32_t* rgba = oo.rgba ? oo.rgba : s->d_canvas;
-    if ((r = launch_trace(s, oo, st, rgba, nullptr, -1, -1, timed)) != RT_OK) return r;
+    if ((r = launch_trace(s, oo, st, rgba, nullptr, -1, -1, timed, -1, te ? te[2] : nullptr, te ? te[3] : nullptr)) != RT_OK) {
+        if (te) s->tev_used -= 4;
+        return r;
+    }
     if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
-    if (te) HIPCHK(hipEventRecord(te[2], st));
     if (o->sync || timed || o->host_outputs) HIPCHK(hipStreamSynchronize(st));
     if (o->host_outputs) {
         if (o->rgba) HIPCHK(hipMemcpy(o->rgba, oo.rgba, out_px * 4, hipMemcpyDeviceToHost));
@@ -2053,16 +2082,16 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
 int rt_timing_collect(rt_scene* s, double* bvh_ms, double* trace_ms, int* n) {
     CHECK_FINISHED(s);
     double a = 0, b = 0;
-    for (size_t i = 0; i + 3 <= s->tev_used; i += 3) {
-        HIPCHK(hipEventSynchronize(s->tev[i + 2]));
+    for (size_t i = 0; i + 4 <= s->tev_used; i += 4) {
+        HIPCHK(hipEventSynchronize(s->tev[i + 3]));
         float x = 0, y = 0;
         HIPCHK(hipEventElapsedTime(&x, s->tev[i], s->tev[i + 1]));
-        HIPCHK(hipEventElapsedTime(&y, s->tev[i + 1], s->tev[i + 2]));
+        HIPCHK(hipEventElapsedTime(&y, s->tev[i + 2], s->tev[i + 3]));
         a += x; b += y;
     }
     if (bvh_ms) *bvh_ms = a;
     if (trace_ms) *trace_ms = b;
-    if (n) *n = (int)(s->tev_used / 3);
+    if (n) *n = (int)(s->tev_used / 4);
     s->tev_used = 0;
     return RT_OK;
 }

@@ -117,8 +117,9 @@ typedef struct rt_render_opts {
     int32_t* hit_tri;   /* primary hit of sample 0: global triangle index, -1 on miss */
     int sync;           /* 1: wait for completion before returning (required for stats) */
     int host_outputs;   /* 1: rgba/radiance/hit_* are HOST pointers; results are copied back (implies sync) */
-    int timing;         /* 1: record device events around the BVH build and the trace kernel on the
-                           launch stream (no sync); totals via rt_timing_collect */
+    int timing;         /* 1: time the BVH build and the trace kernel with start/stop events on the
+                           dispatches themselves (hipExtLaunchKernel; no marker packets, no sync);
+                           totals via rt_timing_collect */
     int textures;       /* 1: textured shading (build-defined, parity-unpinned): the diffuse colour of a
                            hit on a triangle with texture coordinates is its atlas texel instead of Kd
                            (the TODO branch of phong.cu:18-23).  0 (default) = the reference. */

@@ -176,3 +176,26 @@ def test_fast_kernel_exact_grazing_rays(gpu):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, yaw, k)
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+
+
+def test_timed_frames(gpu):
+    """timing=1 (events on the dispatches themselves): one duration pair per frame, both
+    positive, a frame without a BVH rebuild has a zero-length build span, and the image
+    is the one an untimed render produces."""
+    import torch
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 192, 128)
+    ref = s.render(spp=2, want=("rgba",), stats=False)["rgba"]
+    buf = torch.zeros((128, 192), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    s.timing_collect()
+    for f in range(3):
+        s.render_device(spp=2, rebuild_bvh=(f < 2), rgba_ptr=buf.data_ptr(), stream=stream, timing=True)
+    tm = s.timing_collect()
+    assert tm["frames"] == 3
+    assert tm["bvh_ms_total"] > 0 and tm["trace_ms_total"] > 0
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    s.render_device(spp=2, rebuild_bvh=False, rgba_ptr=buf.data_ptr(), stream=stream, timing=True)
+    one = s.timing_collect()
+    assert one["frames"] == 1 and one["bvh_ms_total"] < 0.01 and one["trace_ms_total"] > 0
+    assert s.timing_collect()["frames"] == 0
