@@ -52,9 +52,9 @@ namespace {
 constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
 constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
 #ifndef RT_BLOCK
-#define RT_BLOCK 768
+#define RT_BLOCK 1024
 #endif
-constexpr int TRACE_BLOCK_P = RT_BLOCK;  // persistent block: 12 waves (3 per SIMD, 168-VGPR budget) sharing one LDS BVH copy
+constexpr int TRACE_BLOCK_P = RT_BLOCK;  // persistent block: 16 waves (4 per SIMD, 128-VGPR budget) sharing one LDS BVH copy
 constexpr int LDS_LIMIT = 150 * 1024;    // above this the BVH is read from global memory
 constexpr int PARK_LDS_LIMIT = 158 * 1024;   // BVH image + parking area (160 KB per CU)
 #ifndef RT_NQ
@@ -69,6 +69,19 @@ __device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b 
 // powf of the reference (nvcc pow(float,float)); evaluated in double and rounded:
 // agrees with glibc powf except for 1-ulp cases.
 __device__ __noinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }   // rare: kept out of line
+// pow_ref with the C99 / IEEE special cases that dominate the shading calls answered
+// inline (every powf and pow agree on them bit for bit, F.9.4.4): pow(x, +-0) = 1 (the
+// materials without "alpha"), pow(1, y) = 1, pow(+-0, y > 0) = +0 except -0 for odd integer
+// y (lights behind the surface give max(dot, 0) = +-0).  A wave skips the double-precision
+// call when none of its lanes needs it.
+__device__ __forceinline__ float pow_fast(float x, float y) {
+    if (y == 0.0f || x == 1.0f) return 1.0f;
+    if (x == 0.0f && y > 0.0f) {
+        const bool odd = y == rintf(y) && rintf(0.5f * y) != 0.5f * y;
+        return (odd && signbit(x)) ? -0.0f : 0.0f;
+    }
+    return pow_ref(x, y);
+}
 
 
 
@@ -86,6 +99,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     int n_leaf, n_inst, n_lights, use_bvh;
     int ident_all;            // every instance and mesh rotation is the identity (cube worlds)
     float prune_abs;          // distance-pruning slack M0 (< 0: pruning off), see closest_hit
+    const TriAx* tri_ax;      // axis-plane triangle records (fast kernel; null unless ident_all)
 };
 
 // Parts of a DTri (rt_scene.h): the plane filter's 32-B head and the rest of the test.
@@ -148,6 +162,10 @@ struct BvhRefs {
 #ifndef RT_FILTERED
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
+#ifndef RT_PK_PAIR
+#define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
+                             //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
@@ -171,7 +189,20 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
     auto exact = [&](int c) {
         return c == 0 ? box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) : box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r);
     };
-#if RT_FILTERED
+#if RT_FILTERED && !RT_PK_PAIR
+    // per-child f32 slabs (no splat register copies; see RT_PK_PAIR)
+    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
+        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
+        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
+        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
+        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
+        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
+    };
+    float lo0, hi0, lo1, hi1;
+    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
+    const f2 lo{lo0, lo1}, hi{hi0, hi1};
+#elif RT_FILTERED
     const f2 mnx{A.x, A.y}, mny{A.z, A.w}, mnz{B.x, B.y}, mxx{B.z, B.w}, mxy{C.x, C.y}, mxz{C.z, C.w};
     const f2 ix = splat(ri.ix), iy = splat(ri.iy), iz = splat(ri.iz);
     const f2 bx = splat(ri.bx), by = splat(ri.by), bz = splat(ri.bz);
@@ -180,6 +211,8 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
     const f2 qz0 = __builtin_elementwise_fma(mnz - splat(r.o.z), iz, -bz), qz1 = __builtin_elementwise_fma(mxz - splat(r.o.z), iz, bz);
     const f2 lo = vmax(vmax(vmin(qx0, qx1), vmin(qy0, qy1)), vmin(qz0, qz1));
     const f2 hi = vmin(vmin(vmax(qx0, qx1), vmax(qy0, qy1)), vmax(qz0, qz1));
+#endif
+#if RT_FILTERED
     const f2 el{fabsf(lo.x) * FILT_BOX + FILT_ABS, fabsf(lo.y) * FILT_BOX + FILT_ABS};
     const f2 eh{fabsf(hi.x) * FILT_BOX + FILT_ABS, fabsf(hi.y) * FILT_BOX + FILT_ABS};
     const f2 sep = (lo + el) - (hi - eh);                     // > 0 certainly lo > hi; <= 0 certainly lo <= hi
@@ -232,7 +265,10 @@ __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv,
 // two pose changes depends on the ray only: it is computed once per query by the same
 // operations (qrot_identity, len, the Ray ctor's normalisation), so every leaf sees
 // the same bits it would compute itself; only the origin chain is per leaf.
-struct DirPre { V3 mrd; float scale, dir_len; };
+// `inv` (axis-plane triangles, axis_plane_t): fl(1/mrd_a), NaN where |mrd_a| < 1e-5.
+struct DirPre { V3 mrd, inv; float scale, dir_len; };
+__device__ __forceinline__ float axis_inv(float d) { return fabsf(d) < THRESH ? __builtin_nanf("") : 1.0f / d; }
+template <bool AXIS = false>
 __device__ __forceinline__ DirPre dir_pre(V3 d) {
     DirPre p;
     const V3 ld = qrot_identity(d);                          // Entity::vec_to_local, identity pose
@@ -241,13 +277,18 @@ __device__ __forceinline__ DirPre dir_pre(V3 d) {
     const V3 md = qrot_identity(lrd);                        // HitHandle::get_local_ray, identity mesh pose
     p.scale = len(md);
     p.mrd = normalized(md);
+    if (AXIS) p.inv = v3(axis_inv(p.mrd.x), axis_inv(p.mrd.y), axis_inv(p.mrd.z));
     return p;
 }
+
+// Component `a` of a vector (a wave-uniform axis index: the selects fold into branches).
+__device__ __forceinline__ float comp(V3 v, int a) { return a == 0 ? v.x : a == 1 ? v.y : v.z; }
 
 // t_lo: lower bound of any acceptable local time (-inf if none): the leaf box's entry
 // distance minus the pruning slack M (closest_hit).  A triangle whose plane crossing is
 // certainly below it lies outside the box, so its inside test is skipped.
-template <bool STATS>
+// AXIS: the axis-plane triangle path (S.tri_ax, pre.inv set; identity rotations only).
+template <bool STATS, bool AXIS = false>
 __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b,
                                            const DirPre& pre, WaveCounters& wc, float t_lo) {
     int mesh_id;
@@ -271,6 +312,47 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
     int best = -1;
     float bu = 0.0f, bv_ = 0.0f, t_best = b.time;
 #if RT_FILTERED
+    if (AXIS) {
+        // Axis-plane path (fast kernel, identity rotations): exact plane time from the
+        // per-query reciprocal (axis_plane_t), then the exact in-plane reject (TriAx);
+        // general triangles take the filtered test below.  Same decisions, same order.
+        const float lo = fmaxf(THRESH, t_lo);
+        for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
+            const TriAx x = ldc(S.tri_ax, t);
+            const int ax = x.code & 3;
+            float time, u, v;
+            if (ax == 3) {                                    // general triangle
+                const TriHot h = ld_hot(S.tris, t);
+                float denom, num;
+                const bool pass = tri_plane_f(h.a, h.pn, mr, t_best, t_lo, denom, num);
+                if (!__ballot(pass)) continue;
+                const TriRest q = ld_rest(S.tris, t);
+                if (pass && tri_inside_f(h.a, q.b, q.c, q.area, q.inv_area, mr, t_best, denom, num, time, u, v)) {
+                    t_best = time; best = t; bu = u; bv_ = v;
+                }
+                continue;
+            }
+            const int au = ax == 2 ? 0 : ax + 1, av = ax == 0 ? 2 : ax - 1;
+            const float tt = axis_plane_t(x.a_ax, comp(mr.o, ax), comp(pre.inv, ax));
+            bool pass = tt >= lo && tt < t_best;
+            if (!__ballot(pass)) {
+                if (x.code & 4) t++;                          // same plane, same t, same best: rejected too
+                continue;
+            }
+            if (x.code & 8) {                                 // in-plane reject (TriAx)
+                const float pu = comp(mr.o, au) + tt * comp(mr.d, au), pv = comp(mr.o, av) + tt * comp(mr.d, av);
+                const float pa = comp(mr.o, ax) + tt * comp(mr.d, ax);
+                const float e = fmaxf(fmaxf(x.ulo - pu, pu - x.uhi), fmaxf(x.vlo - pv, pv - x.vhi));
+                pass = pass && !(e > 0.0f && e <= x.win && fabsf(pa - x.a_ax) <= x.off);
+                if (!__ballot(pass)) continue;
+            }
+            const TriHot h = ld_hot(S.tris, t);
+            const TriRest q = ld_rest(S.tris, t);
+            if (pass && tri_inside_t(h.a, q.b, q.c, q.area, q.inv_area, mr, tt, time, u, v)) {
+                t_best = time; best = t; bu = u; bv_ = v;
+            }
+        }
+    } else
     // The plane filter needs only the 32-B head (pn, a) of each record (one batch of
     // scalar loads); the rest is read only for triangles that pass it.
     for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
@@ -348,7 +430,7 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 //    change Light::attenuate (light.cu:35-58).
 //  * triangle skip (cast_local's t_lo): a triangle whose plane crossing is certainly
 //    before tlo(leaf) - M cannot be accepted, so its inside test is not run.
-template <bool NOLEAF, bool STATS, bool FT = false>
+template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
@@ -390,71 +472,75 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // leaf B as -2 - parent, whose pair test is re-run when it is popped (fresh hit
         // and entry bound under the current cut).  Pruning and triangle skip as above.
         DirPre pre{};
-        if (S.ident_all) pre = dir_pre(r.d);
+        if (AXIS) pre = dir_pre<true>(r.d);                      // S.tri_ax set: identity rotations
+        else if (S.ident_all) pre = dir_pre(r.d);
         const bool box_bound = S.prune_abs >= 0.0f;
         auto t_low = [&](float tl) { return box_bound ? tl - slack(tl) : -INFINITY; };
-        auto leaf_i = [&](bool h, int ti, float tl) {
-            if (!__ballot(h)) return;
-            ti = uni(ti);
-            if (h && cast_local<false>(S, bv, ti, r, b, pre, wc, t_low(tl))) {
-                hit = true;
-                if (b.time <= occl_t) active = false;
-            }
-        };
-        int node = 0, sp = 0, stk = 0;
+        // One pair-test site and one leaf site (the leaf code is the bulk of the kernel):
+        // an iteration tests a node's pair -- or, for a popped pending leaf B, re-tests its
+        // parent's pair for child B only -- then runs at most one leaf; when both children
+        // are leaves, B waits in registers (h2, t2, inst2) for the next iteration.
+        int node = 0, sp = 0, stk = 0, bonly = 0, has2 = 0, inst2 = 0;
+        bool h2 = false;
+        float t2 = 0.0f;
         const int my_lane = __lane_id();
         auto push = [&](int e) { stk = my_lane == sp ? e : stk; sp++; };   // v_writelane
         for (;;) {
-            const float4* rec = bv.fnode + 4 * node;
-            bool h0, h1;
-            float t0, t1;
-            pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
-            const float4 rf = rec[3];
-            const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
-            if (prune) {
-                const float ct = cut();
-                h0 = h0 && !(t0 > ct);
-                h1 = h1 && !(t1 > ct);
-            }
-            bool goA = false, goB = false;
-            if (ra < 0) leaf_i(h0, -1 - ra, t0);
-            else goA = __ballot(h0) != 0;
-            if (rb < 0) {
-                const bool hb = h1 && !(prune && t1 > cut());
-                if (goA) {
-                    if (__ballot(hb)) push(-2 - node);
-                } else {
-                    leaf_i(hb, -1 - rb, t1);
-                }
+            bool lh = false;
+            float ltl = 0.0f;
+            int linst = -1;                                    // leaf of this iteration (uniform), -1: none
+            if (has2) {                                        // leaf B right after leaf A (fresh cut)
+                lh = h2 && !(prune && t2 > cut());
+                ltl = t2; linst = inst2; has2 = 0;
             } else {
-                goB = __ballot(h1) != 0;
-            }
-            if (!__ballot(active)) break;                      // every lane occluded
-            if (goA) {
-                if (goB) push(rb);
-                node = ra;
-                continue;
-            }
-            if (goB) { node = rb; continue; }
-            bool more = false;                                 // pop: pending leaves run, an internal node resumes
-            while (sp > 0) {
-                sp--;
-                const int e = __builtin_amdgcn_readlane(stk, sp);
-                if (e < 0) {                                   // leaf B of node -2 - e
-                    const float4* pr = bv.fnode + 4 * (-2 - e);
-                    bool g0, g1;
-                    float u0, u1;
-                    pair_hit_at(pr, r, ri, active, g0, g1, u0, u1);
-                    const int lb = uni(__float_as_int(pr[3].y));
-                    leaf_i(g1 && !(prune && u1 > cut()), -1 - lb, u1);
-                    if (!__ballot(active)) break;
+                const float4* rec = bv.fnode + 4 * node;
+                bool h0, h1;
+                float t0, t1;
+                pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
+                const float4 rf = rec[3];
+                const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
+                if (prune) {
+                    const float ct = cut();
+                    h0 = h0 && !(t0 > ct);
+                    h1 = h1 && !(t1 > ct);
+                }
+                const int bo = bonly;                          // child B only (popped leaf B)
+                bonly = 0;
+                const bool goA = !bo && ra >= 0 && __ballot(h0) != 0;
+                const bool goB = rb >= 0 && __ballot(h1) != 0;
+                if (!bo && ra < 0) { lh = h0; ltl = t0; linst = -1 - ra; }
+                if (rb < 0) {
+                    if (goA) {
+                        if (__ballot(h1)) push(-2 - node);
+                    } else if (linst >= 0) {
+                        h2 = h1; t2 = t1; inst2 = -1 - rb; has2 = 1;
+                    } else {
+                        lh = h1; ltl = t1; linst = -1 - rb;
+                    }
+                }
+                if (goA) {
+                    if (goB) push(rb);
+                    node = ra;
                     continue;
                 }
-                node = e;
-                more = true;
-                break;
+                if (goB) {
+                    if (linst < 0) { node = rb; continue; }
+                    push(rb);                                  // internal B after leaf A
+                }
             }
-            if (!more) break;
+            if (linst >= 0 && __ballot(lh)) {
+                if (lh && cast_local<false, AXIS>(S, bv, uni(linst), r, b, pre, wc, t_low(ltl))) {
+                    hit = true;
+                    if (b.time <= occl_t) active = false;
+                }
+                if (!__ballot(active)) break;                  // every lane occluded
+            }
+            if (has2) continue;
+            if (sp == 0) break;
+            sp--;                                              // pop: an internal node, or leaf B of node -2 - e
+            const int e = __builtin_amdgcn_readlane(stk, sp);
+            if (e < 0) { node = -2 - e; bonly = 1; }
+            else node = e;
         }
         return hit;
     }
@@ -538,7 +624,7 @@ __device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V
     V4 diffuse = nd * kd;
     V3 reflected = reflect(neg(to_light), nrm);
     float rd = dot(neg(reflected), ray_dir);
-    V4 specular = pow_ref(max_std(rd, 0.0f), m.alpha) * m.Ks;
+    V4 specular = pow_fast(max_std(rd, 0.0f), m.alpha) * m.Ks;
     return (diffuse + specular) * incoming;
 }
 
@@ -636,7 +722,7 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
 constexpr int PARK_FIELDS = 25;
-template <int NS, bool STATS, bool PARK, bool TEX, bool FT>
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     Frame cur;
@@ -760,7 +846,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        const bool hit = closest_hit<false, STATS, FT>(S, bv, need, q, b, wc, occl, lim);
+        const bool hit = closest_hit<false, STATS, FT, AXIS>(S, bv, need, q, b, wc, occl, lim);
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -802,8 +888,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             if (cur.depth > 0) {                                   // scene.cu:109-121
                 if (cur.in_obj) {
                     const V4 kt = S.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
-                    cur.atten = cur.atten * v4(pow_ref(is_time, kt.x), pow_ref(is_time, kt.y),
-                                               pow_ref(is_time, kt.z), pow_ref(is_time, kt.w));
+                    cur.atten = cur.atten * v4(pow_fast(is_time, kt.x), pow_fast(is_time, kt.y),
+                                               pow_fast(is_time, kt.z), pow_fast(is_time, kt.w));
                 }
                 cur.type = F_REFLECT;
                 cur.last_mat = is_mat;
@@ -825,8 +911,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 att = v4(0, 0, 0, 0);
             } else {
                 if (dot(hn, q.d) > 0) {                            // calc_shadow_atten (light.cu:18-25)
-                    rv = rv * v4(pow_ref(m.Kt.x, b.time), pow_ref(m.Kt.y, b.time), pow_ref(m.Kt.z, b.time),
-                                 pow_ref(m.Kt.w, b.time));
+                    rv = rv * v4(pow_fast(m.Kt.x, b.time), pow_fast(m.Kt.y, b.time), pow_fast(m.Kt.z, b.time),
+                                 pow_fast(m.Kt.w, b.time));
                 }
                 q = make_ray(at(q, b.time), q.d);
                 max_t -= b.time;
@@ -896,11 +982,12 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // PARK_FIELDS x 4 B x TRACE_BLOCK_P of LDS beside the BVH image.
 // MODE bit 3 (TEX): textured shading (hit_kd), generic frame depth only.
 // MODE bit 4 (FT): traverse the ordered LBVH (closest_hit) instead of the reference heap.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16;
+// MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr bool FT = (MODE & M_FT) != 0;
+    constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
     const BvhRefs bv = stage_bvh<LDS, FT>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
@@ -965,7 +1052,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             }
             if (rd == 0) request(qi);                          // next ticket, in flight during the trace
             const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
             if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             for (int s = 0; s < L; s++) {                      // in-order reduction over samples
@@ -1311,6 +1398,7 @@ struct rt_scene {
     float4* d_node_pair = nullptr; int* d_leaf = nullptr;
     float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
     float4* d_inst4 = nullptr;
+    TriAx* d_tri_ax = nullptr;                   // axis-plane triangle records (tri_axis_records)
     int* d_work = nullptr; int n_cu = 0;
     bool work_zeroed = false;                    // bvh_build_kernel zeroed d_work for the next trace launch
     // longest-first scheduling history (TraceParams::hist): double-buffered by frame parity
@@ -1353,6 +1441,73 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
 }
 
 int upload_inst4(rt_scene* s);
+
+// TriAx records (rt_math.h) of the axis-plane triangle path: axis, plane coordinate,
+// shared-plane flag and the in-plane reject box with its host-checked error bound.
+std::vector<TriAx> tri_axis_records(const rt::Scene& h) {
+    const double u = 0x1p-24;
+    std::vector<TriAx> out(h.d_tris.size());
+    auto c3 = [](V3 v, int a) { return a == 0 ? v.x : a == 1 ? v.y : v.z; };
+    for (size_t i = 0; i < h.d_tris.size(); i++) {
+        const DTri& T = h.d_tris[i];
+        TriAx x{};
+        x.code = 3;
+        int ax = -1, zeros = 0;
+        for (int a = 0; a < 3; a++) {
+            const float c = c3(T.pn, a);
+            if (c == 0.0f) zeros++;                          // +0 or -0
+            else if (c == 1.0f || c == -1.0f) ax = a;
+        }
+        if (zeros == 2 && ax >= 0 && c3(T.b, ax) == c3(T.a, ax) && c3(T.c, ax) == c3(T.a, ax)) {
+            x.code = ax;
+            x.a_ax = c3(T.a, ax);
+            const int au = (ax + 1) % 3, av = (ax + 2) % 3;
+            const V3 P[3] = {T.a, T.b, T.c};
+            double D = 0, lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+            for (int k = 0; k < 3; k++) {
+                const V3 p = P[k], q = P[(k + 1) % 3];
+                const double dx = (double)p.x - q.x, dy = (double)p.y - q.y, dz = (double)p.z - q.z;
+                D = std::max(D, std::sqrt(dx * dx + dy * dy + dz * dz));
+                const double pc[2] = {c3(p, au), c3(p, av)};
+                for (int j = 0; j < 2; j++) { lo[j] = std::min(lo[j], pc[j]); hi[j] = std::max(hi[j], pc[j]); }
+            }
+            // exact (double) doubled area vs the stored float area
+            const double e1[3] = {(double)T.b.x - T.a.x, (double)T.b.y - T.a.y, (double)T.b.z - T.a.z};
+            const double e2[3] = {(double)T.c.x - T.a.x, (double)T.c.y - T.a.y, (double)T.c.z - T.a.z};
+            const double cx = e1[1] * e2[2] - e1[2] * e2[1], cy = e1[2] * e2[0] - e1[0] * e2[2], cz = e1[0] * e2[1] - e1[1] * e2[0];
+            const double A = std::sqrt(cx * cx + cy * cy + cz * cz);
+            const double m = 1e-4 * D, win = 1e3 * D, off = m;
+            bool ok = A > 0 && D > 0 && std::isfinite(A) && std::isfinite(D) && std::isfinite(win);
+            if (ok) {
+                const double eta = std::fabs((double)T.area - A) / A + 1e-12;
+                auto margin = [&](double e) {
+                    return (e / D) * (1 - 5.6 * u - eta) - (5.6 * u + eta) - 41.8 * u * (D + e + off) * (D + e + off) / A - 1.01e-5;
+                };
+                ok = margin(m) > 0 && margin(win) > 0;
+            }
+            if (ok) {
+                // bounds rounded outwards to float
+                x.ulo = std::nextafter((float)(lo[0] - m), -INFINITY); x.uhi = std::nextafter((float)(hi[0] + m), INFINITY);
+                x.vlo = std::nextafter((float)(lo[1] - m), -INFINITY); x.vhi = std::nextafter((float)(hi[1] + m), INFINITY);
+                x.win = std::nextafter((float)win, 0.0f);
+                x.off = std::nextafter((float)off, 0.0f);
+                x.code |= 8;
+            }
+        }
+        out[i] = x;
+    }
+    // shared plane with the next triangle of the same mesh
+    for (const DMesh& M : h.d_meshes)
+        for (int t = M.tri_begin; t + 1 < M.tri_begin + M.tri_count; t++) {
+            const TriAx &x = out[t], &y = out[t + 1];
+            if ((x.code & 3) != 3 && (x.code & 3) == (y.code & 3)) {
+                uint32_t bx, by;
+                memcpy(&bx, &x.a_ax, 4); memcpy(&by, &y.a_ax, 4);
+                if (bx == by) out[t].code |= 4;
+            }
+        }
+    return out;
+}
 
 // Leaf count and depth (internal nodes on the longest root-leaf path) of the ordered
 // LBVH bvh_build_kernel will build: the same box, Morton and sort arithmetic on the
@@ -1434,6 +1589,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_work, 16 * (NQ + 1) * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
+    if ((r = up(s->d_tri_ax, tri_axis_records(h))) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_stats, 24 * sizeof(unsigned long long)));
@@ -1579,6 +1735,10 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     const float radius = pmax + vmax + amax(s->h.d_cam.pos) + 1.0f;
     prune_ok = prune_ok && std::isfinite(radius);
     v.prune_abs = prune_ok ? 4e-4f * vmax + 0x1p-14f * radius : -1.0f;
+#ifndef RT_NO_AXIS
+#define RT_NO_AXIS 0         // 1: A/B variant without the axis-plane triangle path
+#endif
+    v.tri_ax = (!RT_NO_AXIS && v.ident_all && !s->h.d_tris.empty()) ? s->d_tri_ax : nullptr;
     return v;
 }
 
@@ -1660,6 +1820,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
     if (tex) {
         fn = textured[use_lds ? 1 : 0][mode];
+    } else if (ft && park && S.tri_ax) {
+        constexpr int PA = M_PARK | M_FT | M_AXIS;
+        fn = ns <= 0 ? (const void*)trace_kernel<0, true, PA> : ns <= 2 ? (const void*)trace_kernel<2, true, PA>
+                                                                 : (const void*)trace_kernel<NG, true, PA>;
     } else if (ft) {
         constexpr int PF = M_PARK | M_FT;
         fn = park ? (ns <= 0 ? (const void*)trace_kernel<0, true, PF> : ns <= 2 ? (const void*)trace_kernel<2, true, PF>
@@ -1707,7 +1871,7 @@ rt_scene::~rt_scene() {
     dfree(d_fnode);
     for (int p = 0; p < 2; p++) { dfree(d_hlist[p]); dfree(d_hflag[p]); }
     dfree(d_hctl);
-    dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights);
+    dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights); dfree(d_tri_ax);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
     for (auto& p : d_out) dfree(p);

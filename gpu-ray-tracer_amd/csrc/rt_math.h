@@ -309,10 +309,10 @@ RT_HD bool tri_plane_f(V3 a, V3 pn, const Ray& r, float best, float lo, float& d
     float et = fabsf(ta) * FILT_TRI + FILT_ABS;
     return !(ta + et < fmaxf(THRESH, lo) || ta - et >= best);   // false: certainly rejected
 }
-RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray& r, float best, float denom,
-                        float num, float& time, float& u, float& v) {
-    float t = (1.0f / denom) * num;                       // exact (geometry.h:259)
-    if (!(t >= THRESH && t < best)) return false;
+// Inside test of a plane crossing at the exact reference time t (already known to satisfy
+// 1e-5 <= t < best): geometry.h:280-286, filtered.
+RT_HD bool tri_inside_t(V3 a, V3 b, V3 c, float area, float inv_area, const Ray& r, float t, float& time, float& u,
+                        float& v) {
     V3 p = at(r, t);
     V3 x0 = cross(c - p, b - p), x1 = cross(c - p, a - p), x2 = cross(a - p, b - p);
     float s0 = dot(x0, x0), s1 = dot(x1, x1), s2 = dot(x2, x2);
@@ -325,6 +325,40 @@ RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray&
     if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
     return false;
 }
+RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray& r, float best, float denom,
+                        float num, float& time, float& u, float& v) {
+    float t = (1.0f / denom) * num;                       // exact (geometry.h:259)
+    if (!(t >= THRESH && t < best)) return false;
+    return tri_inside_t(a, b, c, area, inv_area, r, t, time, u, v);
+}
+
+// Axis-plane triangles (every cube face): the three vertices share coordinate `ax`
+// exactly and the stored plane normal pn is exactly +-e_ax (two +-0 components).  Then
+// the reference's plane arithmetic collapses without rounding: dot(r.d, pn) = +0 + ... =
+// s * d_ax and dot(a - r.o, pn) = s * fl(a_ax - o_ax) with s = sign(pn_ax) (the +-0
+// products add to +0, and x + 0 = x), and fl(1/(s d)) = s fl(1/d), so
+//   t = fl(fl(1/denom) * num) = fl(fl(1/d_ax) * fl(a_ax - o_ax))     (geometry.h:255-259)
+// bit for bit, and |denom| < 1e-5 <=> |d_ax| < 1e-5.  `inv_ax` carries fl(1/d_ax), or NaN
+// when |d_ax| < 1e-5 (the reference rejects: every comparison with NaN fails).
+RT_HD float axis_plane_t(float a_ax, float o_ax, float inv_ax) { return inv_ax * (a_ax - o_ax); }
+
+// Host-built record of a triangle for the axis-plane path (rt_kernels.hip, cast_local).
+// code: bits 0-1 axis (3 = general triangle), bit 2 = the next triangle of the mesh has the
+// same axis and plane coordinate (identical t: when no lane accepts this plane crossing, the
+// next one is rejected too), bit 3 = the in-plane reject below is valid for this triangle.
+// [ulo, uhi] x [vlo, vhi]: the triangle's extent along the two in-plane axes (u = ax+1,
+// v = ax+2 mod 3) grown by m = 1e-4 D (D = longest edge); win = 1e3 D; off = m.
+// In-plane reject (exact): the point p = at(r, t) fails the reference's inside test when its
+// in-plane excess e = max(ulo - p_u, p_u - uhi, vlo - p_v, p_v - vhi) has 0 < e <= win and
+// |p_ax - a_ax| <= off.  Proof: the exact barycentric weights of p's projection satisfy
+// sum|l_i| - 1 >= e / D (the set sum|l_i| - 1 <= k is the triangle grown about itself by at
+// most k D per side); lifting p off the plane only enlarges the three areas; the reference's
+// float evaluation (differences, cross products, squared norm, sqrt, division by the stored
+// area A~ = A (1 + eta), two additions) differs from the exact sum S by at most
+// 41.8 u M^2 / A + (5.6 u + eta) S with M <= D + e + off.  The host checks
+// (e/D)(1 - 5.6u - eta) - (5.6u + eta) - 41.8 u (D + e + off)^2 / A > 1.01e-5 at e = m and
+// e = win; the left side is concave in e, so it holds on the whole range.
+struct TriAx { int code; float a_ax, ulo, uhi, vlo, vhi, win, off; };
 RT_HD bool tri_accept_f(V3 a, V3 b, V3 c, V3 pn, float area, float inv_area, const Ray& r, float best,
                         float& time, float& u, float& v) {
     float denom, num;

@@ -178,6 +178,27 @@ def test_fast_kernel_exact_grazing_rays(gpu):
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
 
 
+def test_fast_kernel_exact_random_cameras(gpu):
+    """Fast kernel (ordered LBVH, pruning, axis-plane triangle path with its shared-plane
+    skip and in-plane reject) == counted reference-heap kernel, bit for bit, from seeded
+    random camera poses in and around the cube field (any orientation)."""
+    rng = np.random.default_rng(1234)
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 96, 64)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    lit = 0.0
+    for _ in range(16):
+        pos = [float(rng.uniform(-7, 7)), float(rng.uniform(-1, 16)), float(rng.uniform(-7, 7))]
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        s.set_camera(pos, [float(x) for x in q])
+        fast = s.render(spp=2, want=want, stats=False)
+        full = s.render(spp=2, want=want, stats=True)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, k)
+        lit += (full["hit_inst"] >= 0).mean()
+    assert lit / 16 > 0.1
+
+
 def test_timed_frames(gpu):
     """timing=1 (events on the dispatches themselves): one duration pair per frame, both
     positive, a frame without a BVH rebuild has a zero-length build span, and the image
