@@ -1155,16 +1155,42 @@ struct BvhArgs {
     int* work; int n_work;   // the trace kernel's work counters, zeroed here (saves a memset launch)
     unsigned long long* hctl; // next frame's heavy-list counters (2 words), zeroed here too (may be null)
     const DInst* insts; int n_inst;
-    const DMesh* meshes; int n_meshes;
-    const DTri* tris;
+    const Box* mesh_box;     // per-mesh AABB, Trimesh::compute_bounding_box + the mesh pose (host, static)
     int n;                   // padded leaf count (power of two)
-    Box* boxes;              // scratch: n instance boxes
-    Box* tree;               // scratch: 2n-1 boxes, reference storage order
+    Box* tree;               // 2n-1 boxes, reference storage order (global scratch when the LDS cannot hold it)
     float* node_pair;        // out: [12n] child-pair layout (BvhRefs); degenerate boxes: min=+inf, max=-inf
     float4* fnode;           // out: ordered LBVH of the fast kernel, [4 (n_real-1)] (see FNode below)
     int n_real;              // instances with a non-degenerate box (leaves of the ordered LBVH)
     int* leaf_inst;          // out: [n] instance of leaf node n+i
 };
+
+// Box storage of the build: the reference's level arrays (bvh.cu:43-61) as SoA columns
+// (mn xyz, mx xyz, nd) in LDS -- conflict-free for consecutive boxes -- or the global
+// Box array for trees too large for the LDS.
+template <bool LDS_TREE> struct TreeStore;
+template <> struct TreeStore<true> {
+    float* f; int cap;
+    __device__ Box get(int i) const {
+        Box b;
+        b.mn = v3(f[i], f[cap + i], f[2 * cap + i]); b.mx = v3(f[3 * cap + i], f[4 * cap + i], f[5 * cap + i]);
+        b.nd = __float_as_int(f[6 * cap + i]);
+        return b;
+    }
+    __device__ void put(int i, const Box& b) {
+        f[i] = b.mn.x; f[cap + i] = b.mn.y; f[2 * cap + i] = b.mn.z;
+        f[3 * cap + i] = b.mx.x; f[4 * cap + i] = b.mx.y; f[5 * cap + i] = b.mx.z;
+        f[6 * cap + i] = __int_as_float(b.nd);
+    }
+};
+template <> struct TreeStore<false> {
+    Box* t;
+    __device__ Box get(int i) const { return t[i]; }
+    __device__ void put(int i, const Box& b) { t[i] = b; }
+};
+// LDS bytes of bvh_build_kernel<LDS_TREE>: keys u64[n] | idx int[n] | (tree 7 x f32 [2n-1])
+__host__ __device__ inline size_t bvh_lds_bytes(int n, bool lds_tree) {
+    return 12 * (size_t)n + (lds_tree ? 28 * (size_t)(2 * n - 1) : 0);
+}
 
 // Karras radix-tree node i over sorted 64-bit keys k[0, nr): range [first, last] and
 // split gamma (left = [first, gamma], right = [gamma+1, last]); equal keys are told
@@ -1199,38 +1225,38 @@ __host__ __device__ inline void fnode_split(const unsigned long long* k, int nr,
     last = i < j ? j : i;
 }
 
+template <bool LDS_TREE>
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned long long* keys = reinterpret_cast<unsigned long long*>(smem);
     int* idx = reinterpret_cast<int*>(smem + sizeof(unsigned long long) * A.n);
-    Box* mbox = reinterpret_cast<Box*>(smem + 12 * (size_t)A.n);
+    TreeStore<LDS_TREE> tree;
+    if constexpr (LDS_TREE) { tree.f = reinterpret_cast<float*>(smem + 12 * (size_t)A.n); tree.cap = 2 * A.n - 1; }
+    else tree.t = A.tree;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n = A.n;
     for (int i = tid; i < A.n_work; i += nt) A.work[i] = 0;
     if (A.hctl && tid < 2) A.hctl[tid] = 0;
 
-    // mesh boxes: Trimesh::compute_bounding_box (trimesh.cu:21-32), sequential fit order
-    for (int m = tid; m < A.n_meshes; m += nt) {
+    // instance boxes (create_boxes, raytracer.cu:54-74: from_local of the mesh box) and
+    // Morton keys (gen_morton, bvh.cu:20-32); padding is degenerate -> ULONG_MAX
+    auto inst_box = [&](int i) {
         Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
-        const DMesh mesh = A.meshes[m];
-        for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
-            fit_vertex(b, A.tris[t].a); fit_vertex(b, A.tris[t].b); fit_vertex(b, A.tris[t].c);
-        }
-        mbox[m] = from_local(b, mesh.pose);
-    }
-    __syncthreads();
-    // instance boxes + Morton keys (gen_morton, bvh.cu:20-32); padding is degenerate -> ULONG_MAX
+        if (i < A.n_inst) b = from_local(A.mesh_box[A.insts[i].mesh], A.insts[i].pose);
+        return b;
+    };
     for (int i = tid; i < n; i += nt) {
-        Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
-        if (i < A.n_inst) b = from_local(mbox[A.insts[i].mesh], A.insts[i].pose);
-        A.boxes[i] = b;
+        const Box b = inst_box(i);
         keys[i] = b.nd ? z_order(neg(box_center(b))) : ~0ull;
         idx[i] = i;
     }
     __syncthreads();
-    // bitonic sort on (key, index): identical order to a stable sort by key
+    // bitonic sort on (key, index): identical order to a stable sort by key.  Strides >= 64
+    // exchange through the LDS; the strides below 64 of each merge run in registers within
+    // the wave (lane ^ stride), one LDS round trip and barrier per merge instead of per stride.
     for (int size = 2; size <= n; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        int stride = size >> 1;
+        for (; stride >= 64 || (n < 64 && stride > 0); stride >>= 1) {
             for (int i = tid; i < n; i += nt) {
                 int j = i ^ stride;
                 if (j > i) {
@@ -1243,21 +1269,40 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             }
             __syncthreads();
         }
+        if (stride > 0) {                                      // n >= 64: whole waves in range
+            for (int i = tid; i < n; i += nt) {
+                unsigned long long k = keys[i];
+                int x = idx[i];
+                const bool up = (i & size) == 0;
+                for (int st = stride; st > 0; st >>= 1) {
+                    const unsigned lo = __shfl_xor((unsigned)k, st), hi = __shfl_xor((unsigned)(k >> 32), st);
+                    const unsigned long long pk = ((unsigned long long)hi << 32) | lo;
+                    const int px = __shfl_xor(x, st);
+                    const bool mine_less = k < pk || (k == pk && x < px);
+                    if (mine_less != (((i & st) == 0) == up)) { k = pk; x = px; }   // lower lane keeps min iff up
+                }
+                keys[i] = k; idx[i] = x;
+            }
+            __syncthreads();
+        }
     }
-    // reorder (bvh.cu:34-41) and pairwise level merges (bvh.cu:43-61)
-    for (int i = tid; i < n; i += nt) A.tree[i] = A.boxes[idx[i]];
+    // reorder (bvh.cu:34-41: the box is recomputed, same arithmetic) and pairwise level
+    // merges (bvh.cu:43-61)
+    for (int i = tid; i < n; i += nt) tree.put(i, inst_box(idx[i]));
     __syncthreads();
-    int lvl = 0, size = n, out = n;
-    while (size >= 2) {
-        for (int i = tid; i < size / 2; i += nt) A.tree[out + i] = merge(A.tree[lvl + 2 * i], A.tree[lvl + 2 * i + 1]);
-        __syncthreads();
-        lvl += size; out += size / 2; size >>= 1;
+    {
+        int lvl = 0, size = n, out = n;
+        while (size >= 2) {
+            for (int i = tid; i < size / 2; i += nt) tree.put(out + i, merge(tree.get(lvl + 2 * i), tree.get(lvl + 2 * i + 1)));
+            __syncthreads();
+            lvl += size; out += size / 2; size >>= 1;
+        }
     }
     // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
     for (int k = tid; k < 2 * n; k += nt) {
         Box b;
         b.nd = 0;
-        if (k > 0) b = A.tree[2 * n - 1 - k];
+        if (k > 0) b = tree.get(2 * n - 1 - k);
         if (!b.nd) { b.mn = v3(INFINITY, INFINITY, INFINITY); b.mx = v3(-INFINITY, -INFINITY, -INFINITY); }
         float* q = A.node_pair + 12 * (k >> 1) + (k & 1);
         q[0] = b.mn.x; q[2] = b.mn.y; q[4] = b.mn.z; q[6] = b.mx.x; q[8] = b.mx.y; q[10] = b.mx.z;
@@ -1281,8 +1326,8 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             Box b;
             b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
             for (int l = lo[c], r = hi[c] + 1, off = 0, size = n; l < r; l >>= 1, r >>= 1, off += size, size >>= 1) {
-                if (l & 1) b = merge(b, A.tree[off + l++]);
-                if (r & 1) b = merge(b, A.tree[off + --r]);
+                if (l & 1) b = merge(b, tree.get(off + l++));
+                if (r & 1) b = merge(b, tree.get(off + --r));
             }
             q[0 + c] = b.mn.x; q[2 + c] = b.mn.y; q[4 + c] = b.mn.z; q[6 + c] = b.mx.x; q[8 + c] = b.mx.y; q[10 + c] = b.mx.z;
             refs[c] = lo[c] == hi[c] ? -1 - idx[lo[c]] : cl[c];      // leaf: -1 - instance
@@ -1394,7 +1439,7 @@ struct rt_scene {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // device buffers
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
-    DLight* d_lights = nullptr; Box* d_boxes = nullptr; Box* d_tree = nullptr;
+    DLight* d_lights = nullptr; Box* d_mesh_box = nullptr; Box* d_tree = nullptr;
     float4* d_node_pair = nullptr; int* d_leaf = nullptr;
     float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
     float4* d_inst4 = nullptr;
@@ -1513,7 +1558,10 @@ std::vector<TriAx> tri_axis_records(const rt::Scene& h) {
 // LBVH bvh_build_kernel will build: the same box, Morton and sort arithmetic on the
 // host (RT_HD functions).  The fast traversal's stack holds <= FT_MAX_DEPTH entries.
 constexpr int FT_MAX_DEPTH = 31;
-void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
+// Mesh boxes: Trimesh::compute_bounding_box (trimesh.cu:21-32, sequential fit order) and
+// the mesh pose.  They depend only on the immutable mesh data, so they are computed once
+// here; the per-frame build (bvh_build_kernel) redoes everything per instance.
+std::vector<Box> mesh_boxes(const rt::Scene& h) {
     std::vector<Box> mbox(h.d_meshes.size());
     for (size_t m = 0; m < h.d_meshes.size(); m++) {
         Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
@@ -1523,6 +1571,10 @@ void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
         }
         mbox[m] = from_local(b, mesh.pose);
     }
+    return mbox;
+}
+void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
+    const std::vector<Box> mbox = mesh_boxes(h);
     std::vector<std::pair<unsigned long long, int>> kv;
     for (size_t i = 0; i < h.d_insts.size(); i++) {
         const Box b = from_local(mbox[h.d_insts[i].mesh], h.d_insts[i].pose);
@@ -1590,7 +1642,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_work, 16 * (NQ + 1) * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
     if ((r = up(s->d_tri_ax, tri_axis_records(h))) != RT_OK) return r;
-    HIPCHK(hipMalloc((void**)&s->d_boxes, nl * sizeof(Box)));
+    if ((r = up(s->d_mesh_box, mesh_boxes(h))) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
     HIPCHK(hipMalloc((void**)&s->d_stats, 24 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
@@ -1688,21 +1740,22 @@ int build_bvh(rt_scene* s, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e
     }
     BvhArgs A;
     A.insts = s->d_insts; A.n_inst = (int)s->h.d_insts.size();
-    A.meshes = s->d_meshes; A.n_meshes = (int)s->h.d_meshes.size();
-    A.tris = s->d_tris; A.n = s->n_leaf;
-    A.boxes = s->d_boxes; A.tree = s->d_tree;
+    A.mesh_box = s->d_mesh_box; A.n = s->n_leaf;
+    A.tree = s->d_tree;
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     A.fnode = s->d_fnode; A.n_real = s->n_real;
     A.work = s->d_work; A.n_work = 16 * (NQ + 1);
     // the slot the next fast frame records its heavy list into (launch_trace skips its memset)
     A.hctl = s->d_hctl ? s->d_hctl + 2 * (1 - s->hist_parity) : nullptr;
     s->hctl_zeroed = s->d_hctl ? 1 - s->hist_parity : -1;
-    size_t lds = 12 * (size_t)A.n + sizeof(Box) * std::max(1, A.n_meshes);
-    lds = (lds + 15) & ~size_t(15);
+    const bool lds_tree = bvh_lds_bytes(A.n, true) <= 160 * 1024;       // n <= 2048
+    const size_t lds = bvh_lds_bytes(A.n, lds_tree);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
+    const void* fn = lds_tree ? (const void*)bvh_build_kernel<true> : (const void*)bvh_build_kernel<false>;
+    if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     void* args[] = {&A};
     // e0/e1 (timing=1): timestamps taken by the dispatch itself, no marker packets
-    HIPCHK(hipExtLaunchKernel((const void*)bvh_build_kernel, dim3(1), dim3(1024), args, lds, st, e0, e1, 0));
+    HIPCHK(hipExtLaunchKernel(fn, dim3(1), dim3(1024), args, lds, st, e0, e1, 0));
     HIPCHK(hipGetLastError());
     s->bvh_valid = true;
     s->work_zeroed = true;
@@ -1873,7 +1926,7 @@ rt_scene::~rt_scene() {
     dfree(d_hctl);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights); dfree(d_tri_ax);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
-    dfree(d_boxes); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
+    dfree(d_mesh_box); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : tev) (void)hipEventDestroy(e);

@@ -189,19 +189,23 @@ RT_HD bool box_hit(V3 mn, V3 mx, const Ray& r) {
 RT_HD V3 box_center(const Box& b) { return 0.5f * (b.mn + b.mx); }
 
 // z_order.cu:5-36 — 64-bit interleave of the raw float bits, x first, MSB first.
+// The loop emits, MSB first, x bit 31-k at output bit 63-3k (k = 0..21), y bit 31-k at
+// 62-3k and z bit 31-k at 61-3k (k = 0..20); with X = x >> 10, Y = y >> 11, Z = z >> 11
+// that is bit j of X -> 3j, of Z -> 3j+1, of Y -> 3j+2: three magic-mask bit spreads.
+RT_HD uint64_t spread3(uint64_t v) {                 // bit j (j < 21) -> bit 3j
+    v &= 0x1fffffull;
+    v = (v | v << 32) & 0x1f00000000ffffull;
+    v = (v | v << 16) & 0x1f0000ff0000ffull;
+    v = (v | v << 8) & 0x100f00f00f00f00full;
+    v = (v | v << 4) & 0x10c30c30c30c30c3ull;
+    v = (v | v << 2) & 0x1249249249249249ull;
+    return v;
+}
 RT_HD uint64_t z_order(V3 vec) {
     V3 inv = neg(vec);
     union { float f; uint32_t u; } cx{inv.x}, cy{inv.y}, cz{inv.z};
-    uint32_t xo = 31, yo = 31, zo = 31;
-    uint64_t t = 0;
-    for (unsigned i = 0; i < 64; i++) {
-        t <<= 1;
-        unsigned m = i % 3;
-        if (m == 0) { t |= (cx.u >> xo) & 1u; xo--; }
-        else if (m == 1) { t |= (cy.u >> yo) & 1u; yo--; }
-        else { t |= (cz.u >> zo) & 1u; zo--; }
-    }
-    return t;
+    const uint32_t X = cx.u >> 10, Y = cy.u >> 11, Z = cz.u >> 11;   // 22, 21, 21 bits
+    return spread3(X) | ((uint64_t)(X >> 21) << 63) | (spread3(Z) << 1) | (spread3(Y) << 2);
 }
 
 // ---- triangle test (geometry.h:229-290) with ray-independent factors precomputed ----

@@ -23,6 +23,7 @@ def oracle():
 @pytest.fixture(scope="session")
 def rt():
     """The product library; GPU tests require a device (no fallback)."""
+    import torch  # noqa: F401  -- first, so torch and librt_amd.so bind the same HIP runtime
     import rtamd
     rtamd.lib()
     return rtamd
