@@ -7,7 +7,9 @@ Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit que
 
 One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
 rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
-the packed RGBA8 rows to rank 0 and the row un-permute.  The frame stays in HBM
+the packed RGBA8 rows to rank 0 and the row un-permute.  Over RCCL the gather of
+frame k runs on the collective stream while frame k+1 renders (double-buffered
+slices); the timed region ends after the last frame's gather and un-permute.  The frame stays in HBM
 (the PCIe read-back is reported separately as `ms_per_step_with_readback`).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver
@@ -113,16 +115,20 @@ def main():
         scene.load_atlas()
     W, H = scene.width, scene.height
     my_rows = len(rtdist.rows_of(rank, world, H))
-    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo)
+    # RCCL: double-buffered slices, frame k's gather overlaps frame k+1's render (rtamd.dist)
+    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo, slots=2)
     part = fb.part
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
+    frame_no = [0]
 
     def step(timing):
+        k = frame_no[0]
+        frame_no[0] += 1
         scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
-                            compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, timing=timing,
-                            textures=args.textures)
-        fb.gather()
+                            compact=True, rgba_ptr=fb.slot_part(k).data_ptr(), stream=stream.cuda_stream,
+                            timing=timing, textures=args.textures)
+        fb.gather(k)
 
     # per-frame work counters (deterministic): one untimed counted render of this rank's rows
     st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
@@ -132,6 +138,7 @@ def main():
     torch.cuda.synchronize()
     tc = time.perf_counter()
     step(False)
+    fb.finish()
     torch.cuda.synchronize()
     cold_ms = (time.perf_counter() - tc) * 1e3
     for _ in range(max(0, args.warmup - 1)):
@@ -143,6 +150,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(not args.no_kernel_timing)
+    fb.finish()                                             # the last frame's gather + un-permute
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -154,6 +162,7 @@ def main():
     host = None
     for _ in range(max(1, args.steps // 2)):
         step(False)
+        fb.finish()
         if rank == 0:
             host = fb.frame.cpu()
     torch.cuda.synchronize()

@@ -8,6 +8,12 @@ exchange is gathering the packed RGBA8 slices to rank 0 (RCCL `gather` over xGMI
 GPUs; any torch.distributed backend works, the CPU tests use gloo) and the row
 un-permute there.  Slices are padded to ceil(H/G) rows so every message has the
 same size.
+
+Pipelining (`slots=2`, bench.py over RCCL): frame k renders into slice buffer k % 2
+and its gather is issued asynchronously, so it runs on the collective stream while
+frame k+1 renders; frame k's un-permute is enqueued when frame k+1's gather is issued
+(or by `finish()`), after waiting for frame k's gather.  The waits are stream
+dependencies, not host synchronisation.
 """
 import torch
 
@@ -22,32 +28,70 @@ def slice_height(world, height):
 
 
 class RowCyclicFrame:
-    """Per-rank slice buffer + (rank 0) the assembled frame.
+    """Per-rank slice buffer(s) + (rank 0) the assembled frame.
 
     `part` is the compact slice a rank renders into (rt_render_opts.row0 = rank,
     row_step = world, compact = 1); `gather()` assembles the frame on rank 0.
     """
 
-    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, host_staging=False):
+    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, host_staging=False,
+                 slots=1):
         """host_staging: gather through host memory (backends without device tensors,
-        e.g. gloo when testing the multi-rank path on one GPU)."""
+        e.g. gloo when testing the multi-rank path on one GPU).  slots = 2: double-buffered
+        slices with asynchronous gathers (see the module docstring)."""
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.host_staging = host_staging
         self.rows = slice_height(world, height)
-        self.part = torch.zeros((self.rows, width), dtype=dtype, device=device)
+        self.slots = 1 if (world == 1 or host_staging) else max(1, slots)
+        self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(self.slots)]
+        self.part = self.parts[0]
         gdev = "cpu" if host_staging else device
-        self.gathered = ([torch.empty((self.rows, width), dtype=dtype, device=gdev) for _ in range(world)]
-                         if (world > 1 and rank == 0) else None)
+        # rank 0: one contiguous [world, rows, W] buffer; the gather list is its views
+        self.gbuf = (torch.empty((world, self.rows, width), dtype=dtype, device=gdev)
+                     if (world > 1 and rank == 0) else None)
+        self.gathered = list(self.gbuf.unbind(0)) if self.gbuf is not None else None
         # one rank: the slice is the frame (rows_of(0, 1, H) = every row, in order) -- no copy
         self.frame = (self.part if world == 1 else
                       torch.empty((height, width), dtype=dtype, device=device) if rank == 0 else None)
+        self._pending = None
 
-    def gather(self):
-        """Collect every rank's slice on rank 0 and un-permute the rows into `frame`."""
-        if self.world > 1:
-            self.dist.gather(self.part.cpu() if self.host_staging else self.part, self.gathered, dst=0)
+    def slot_part(self, k):
+        """Slice buffer frame k renders into."""
+        return self.parts[k % self.slots]
+
+    def _unpermute(self):
+        if self.H % self.world == 0:       # frame row i*G + r = slice r row i: one strided copy
+            self.frame.view(self.rows, self.world, self.W).copy_(self.gbuf.transpose(0, 1))
+        else:
+            for r in range(self.world):
+                n = len(rows_of(r, self.world, self.H))
+                self.frame[r::self.world] = self.gathered[r][:n].to(self.frame.device)
+
+    def finish(self):
+        """Complete an outstanding asynchronous gather (stream-ordered) and un-permute."""
+        if self._pending is not None:
+            self._pending.wait()
+            self._pending = None
             if self.rank == 0:
-                for r in range(self.world):
-                    n = len(rows_of(r, self.world, self.H))
-                    self.frame[r::self.world] = self.gathered[r][:n].to(self.frame.device)
+                self._unpermute()
+        return self.frame
+
+    def gather(self, k=0):
+        """Collect every rank's slice of frame k on rank 0 and un-permute the rows into
+        `frame`.  With slots = 2 the gather is left in flight (finish() / the next call
+        completes it)."""
+        if self.world == 1:
+            return self.frame
+        self.finish()
+        src = self.slot_part(k)
+        if self.host_staging:
+            self.dist.gather(src.cpu(), self.gathered, dst=0)
+            if self.rank == 0:
+                self._unpermute()
+            return self.frame
+        work = self.dist.gather(src, self.gathered, dst=0, async_op=self.slots > 1)
+        if self.slots > 1:
+            self._pending = work
+        elif self.rank == 0:
+            self._unpermute()
         return self.frame

@@ -20,7 +20,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, scene, w, h, spp, out_path):
+def _rank_main(rank, world, port, scene, w, h, spp, out_path, slots):
     import torch.distributed as dist
     from oracle_lib import Oracle
     import rtamd.dist as rtdist
@@ -30,25 +30,37 @@ def _rank_main(rank, world, port, scene, w, h, spp, out_path):
         orc = Oracle()
         fr = orc.render(orc.load(scene_path(scene), w, h), spp=spp, row0=rank, row_step=world, nthreads=2,
                         want=("rgba",))
-        fb = rtdist.RowCyclicFrame(w, h, world, rank, "cpu", dist)
-        mine = fr["rgba"].view(np.int32)
-        # the oracle returns the full-size frame; take this rank's rows (compact slice)
-        rows = list(rtdist.rows_of(rank, world, h))
-        fb.part[:len(rows)] = torch.from_numpy(np.ascontiguousarray(mine[rows]))
-        out = fb.gather()
+        fb = rtdist.RowCyclicFrame(w, h, world, rank, "cpu", dist, slots=slots)
+        mine = torch.from_numpy(np.ascontiguousarray(fr["rgba"].view(np.int32)[list(rtdist.rows_of(rank, world, h))]))
+        # the oracle returns the full-size frame; each rank takes its rows (compact slice).
+        # Three frames through the (pipelined) gather: frame k = image + k, so a stale
+        # or overwritten slot shows up in the last or the middle frame.
+        outs = []
+        for k in range(3):
+            fb.slot_part(k)[:mine.shape[0]] = mine + k
+            out = fb.gather(k)
+            if k == 1:
+                fb.finish()
+                if rank == 0:
+                    outs.append(out.clone())
+        out = fb.finish()
         if rank == 0:
-            np.save(out_path, out.numpy())
+            np.save(out_path, np.stack([outs[0].numpy(), out.numpy()]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_cyclic_gather_reassembles_frame(oracle, tmp_path, world):
-    scene, w, h, spp = "world8_stress", 96, 61, 2          # 61 rows: ragged last slice for G = 2, 3
+@pytest.mark.parametrize("world,h,slots", [(2, 61, 1), (3, 61, 1), (2, 60, 2), (3, 60, 2), (3, 61, 2)])
+def test_row_cyclic_gather_reassembles_frame(oracle, tmp_path, world, h, slots):
+    """61 rows: ragged last slice (row loop un-permute); 60: one strided copy; slots = 2:
+    double-buffered asynchronous gathers (bench.py's RCCL mode)."""
+    scene, w, spp = "world8_stress", 96, 2
     out_path = str(tmp_path / "frame.npy")
-    mp.spawn(_rank_main, args=(world, _free_port(), scene, w, h, spp, out_path), nprocs=world, join=True)
-    full = oracle.render(oracle.load(scene_path(scene), w, h), spp=spp, nthreads=4, want=("rgba",))
-    assert np.array_equal(np.load(out_path), full["rgba"].view(np.int32))
+    mp.spawn(_rank_main, args=(world, _free_port(), scene, w, h, spp, out_path, slots), nprocs=world, join=True)
+    full = oracle.render(oracle.load(scene_path(scene), w, h), spp=spp, nthreads=4, want=("rgba",))["rgba"].view(np.int32)
+    got = np.load(out_path)
+    assert np.array_equal(got[0], full + 1)
+    assert np.array_equal(got[1], full + 2)
 
 
 def test_rows_partition_covers_frame_once():
