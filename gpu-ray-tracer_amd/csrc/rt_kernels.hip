@@ -162,6 +162,10 @@ struct BvhRefs {
 #ifndef RT_FILTERED
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
+#ifndef RT_TPC
+#define RT_TPC 2             // work indices claimed per ticket (trace_kernel's group loop)
+#endif
+constexpr int TPC = RT_TPC;
 #ifndef RT_PK_PAIR
 #define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
                              //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
@@ -288,7 +292,7 @@ __device__ __forceinline__ float comp(V3 v, int a) { return a == 0 ? v.x : a == 
 // distance minus the pruning slack M (closest_hit).  A triangle whose plane crossing is
 // certainly below it lies outside the box, so its inside test is skipped.
 // AXIS: the axis-plane triangle path (S.tri_ax, pre.inv set; identity rotations only).
-template <bool STATS, bool AXIS = false>
+template <bool STATS, bool AXIS = false, bool PROF = false>
 __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv, int ti, const Ray& r, Best& b,
                                            const DirPre& pre, WaveCounters& wc, float t_lo) {
     int mesh_id;
@@ -321,6 +325,7 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
             const TriAx x = ldc(S.tri_ax, t);
             const int ax = x.code & 3;
             float time, u, v;
+            if (PROF) wc.wtri++;
             if (ax == 3) {                                    // general triangle
                 const TriHot h = ld_hot(S.tris, t);
                 float denom, num;
@@ -346,6 +351,7 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
                 pass = pass && !(e > 0.0f && e <= x.win && fabsf(pa - x.a_ax) <= x.off);
                 if (!__ballot(pass)) continue;
             }
+            if (PROF) { wc.wbary++; wc.lbary += __popcll(__ballot(pass)); }
             const TriHot h = ld_hot(S.tris, t);
             const TriRest q = ld_rest(S.tris, t);
             if (pass && tri_inside_t(h.a, q.b, q.c, q.area, q.inv_area, mr, tt, time, u, v)) {
@@ -430,7 +436,7 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 //    change Light::attenuate (light.cu:35-58).
 //  * triangle skip (cast_local's t_lo): a triangle whose plane crossing is certainly
 //    before tlo(leaf) - M cannot be accepted, so its inside test is not run.
-template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false>
+template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false, bool PROF = false>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
@@ -446,7 +452,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     };
     bool active = active_in;
     const unsigned long long am = __ballot(active);
-    if (STATS) { wc.rays += __popcll(am); wc.wq++; }
+    if (STATS || PROF) { wc.rays += __popcll(am); wc.wq++; }
     bool hit = false;
     if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
         DirPre pre{};
@@ -496,6 +502,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 const float4* rec = bv.fnode + 4 * node;
                 bool h0, h1;
                 float t0, t1;
+                if (PROF) wc.wpair++;
                 pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
                 const float4 rf = rec[3];
                 const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
@@ -529,10 +536,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 }
             }
             if (linst >= 0 && __ballot(lh)) {
-                if (lh && cast_local<false, AXIS>(S, bv, uni(linst), r, b, pre, wc, t_low(ltl))) {
+                const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+                if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
+                if (lh && cast_local<false, AXIS, PROF>(S, bv, uni(linst), r, b, pre, wc, t_low(ltl))) {
                     hit = true;
                     if (b.time <= occl_t) active = false;
                 }
+                if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
                 if (!__ballot(active)) break;                  // every lane occluded
             }
             if (has2) continue;
@@ -646,6 +656,7 @@ struct TraceParams {
     int W, H, row0, row_step, n_rows, compact, spp, depth;
     int lanes_per_px, px_per_wave, gw, gh, n_gx, n_groups;   // sample-parallel lane mapping
     int scramble;             // ticket -> group permutation factor (coprime with the queue length)
+    int scramble_small;       // 1: ticket * scramble < 2^32 for every ticket (32-bit modulo)
     const float2* __restrict__ spp_off;
     uint32_t* rgba;
     float4* radiance;
@@ -722,7 +733,7 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
 constexpr int PARK_FIELDS = 25;
-template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS>
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     Frame cur;
@@ -753,7 +764,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     };
     unsigned long long c_post = 0;
     for (;;) {
-        if (STATS && c_post) { wc.cyc_post += __builtin_amdgcn_s_memtime() - c_post; c_post = 0; }
+        if ((STATS || PROF) && c_post) { wc.cyc_post += __builtin_amdgcn_s_memtime() - c_post; c_post = 0; }
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
             if (st == ST_LIGHT) {
@@ -845,8 +856,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             put(dtl.x); put(dtl.y); put(dtl.z);
             asm volatile("" ::: "memory");
         }
-        const unsigned long long c0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        const bool hit = closest_hit<false, STATS, FT, AXIS>(S, bv, need, q, b, wc, occl, lim);
+        const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
+        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(S, bv, need, q, b, wc, occl, lim);
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -861,7 +872,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             dtl.x = get(); dtl.y = get(); dtl.z = get();
         }
         unsigned long long c1 = 0;
-        if (STATS) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
+        if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
@@ -983,7 +994,9 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 3 (TEX): textured shading (hit_kd), generic frame depth only.
 // MODE bit 4 (FT): traverse the ordered LBVH (closest_hit) instead of the reference heap.
 // MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32;
+// MODE bit 6 (PROF): profiling variant of the fast kernel -- wave-level step counts and
+// s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -993,6 +1006,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
+    constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
     float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
@@ -1011,28 +1025,49 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         if (P.hctl_prev[1]) thr = 4 * P.hctl_prev[1] / (unsigned long long)P.n_groups;
     }
     int qi = n_heavy > 0 ? -1 : 0;                           // -1: the previous frame's heavy groups first
-    // Lane 0 holds the raw result of the pending ticket request.  It is requested after
-    // the group's own global loads (vmcnt retires in order, so an earlier atomic would
-    // hold them up) and read only when the next group starts.
-    int pend = 0;
+    // Lane 0 holds the raw result of the pending ticket request.  A ticket claims TPC
+    // consecutive work indices of its queue (one index in the heavy list); the next one is
+    // requested when the batch's last group starts, after that group's own global loads
+    // (vmcnt retires in order, so an earlier atomic would hold them up), and read when the
+    // batch is used up.  Fewer, batched device-scope atomics: the counters sustain ~100 M
+    // atomics/s each, which alone bounded a TPC = 1 frame at 0.75 ms (measured, group
+    // loop without tracing).
+    int pend = 0, inflight = 0;
+    auto step_of = [&](int q) { return q < 0 ? 1 : TPC; };
     auto request = [&](int q) {
-        if (lane == 0) pend = atomicAdd(q < 0 ? &P.work[16 * NQ] : &P.work[16 * ((q0 + q) % NQ)], 1);
+        if (lane == 0) pend = atomicAdd(q < 0 ? &P.work[16 * NQ] : &P.work[16 * ((q0 + q) % NQ)], step_of(q));
+        inflight = 1;
     };
-    auto resolve = [&]() { return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
+    auto resolve = [&]() { inflight = 0; return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
     request(qi);
-    int ticket = resolve();
-    const unsigned long long c_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    const unsigned long long rt_start = STATS ? __builtin_amdgcn_s_memrealtime() : 0;   // global 100 MHz clock
+    int tbase = resolve(), j = 0;
+    const unsigned long long c_start = CYC ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rt_start = CYC ? __builtin_amdgcn_s_memrealtime() : 0;   // global 100 MHz clock
     for (;;) {
-        while (qi < NQ && ticket >= (qi < 0 ? n_heavy : per_q)) { qi++; if (qi < NQ) { request(qi); ticket = resolve(); } }
+        for (;;) {                                             // next work index tbase + j of queue qi
+            if (qi >= NQ) break;
+            const int lim = qi < 0 ? n_heavy : per_q;
+            if (tbase + j >= lim) {                             // queue drained (a pending batch is past it too)
+                if (inflight) (void)resolve();
+                qi++; j = 0;
+                if (qi < NQ) { request(qi); tbase = resolve(); }
+                continue;
+            }
+            if (j < step_of(qi)) break;
+            if (!inflight) request(qi);                        // batch used up
+            tbase = resolve(); j = 0;
+        }
         if (qi >= NQ) break;
+        const int ticket = tbase + j++;
+        const bool last_of_batch = j == step_of(qi);
         // tickets visit the queue's groups in a scrambled order (t * scramble mod per_q, a
         // bijection): expensive image regions are spread over the frame instead of all
         // starting last and leaving a long tail of idle CUs (measured: first wave done at
         // 69% of the kernel span with row order)
         const int g = qi < 0 ? uni(P.hl_prev[ticket])
-                             : ((q0 + qi) % NQ) + NQ * (int)(((long long)ticket * P.scramble) % per_q);
-        if (g >= P.n_groups || (qi >= 0 && P.hist && P.hf_prev[g])) { request(qi); ticket = resolve(); continue; }
+                             : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)(((unsigned)ticket * (unsigned)P.scramble) % (unsigned)per_q)
+                                                                         : (int)(((long long)ticket * P.scramble) % per_q));
+        if (g >= P.n_groups || (qi >= 0 && P.hist && P.hf_prev[g])) continue;
         const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
         const int gx = g % P.n_gx, gy = g / P.n_gx;
         const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
@@ -1041,7 +1076,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
         const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
-        const unsigned long long g_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
+        const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         for (int rd = 0; rd < rounds; rd++) {
             const int k = rd * L + sub;
             const bool act = valid && k < P.spp;
@@ -1050,16 +1085,24 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
                 float2 o = P.spp_off[k];
                 r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
             }
-            if (rd == 0) request(qi);                          // next ticket, in flight during the trace
-            const unsigned long long cs = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            if (rd == 0 && last_of_batch) request(qi);         // next ticket, in flight during the trace
+            const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
+#if RT_EXP_NOTRACE                                             // experiment: group overhead only
+            V4 c = v4(r0.d.x, r0.d.y, r0.d.z, 1.0f);
+#else
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
-            if (STATS) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
-            for (int s = 0; s < L; s++) {                      // in-order reduction over samples
+#endif
+            if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
+            auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
+                return v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y, v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);
+            };
+            // in-order reduction over samples (ds_bpermute: the LDS pipe has room, the VALU
+            // does not -- a DPP row-shift form measured 4% slower)
+            for (int s = 0; s < L; s++) {
                 V4 v = shfl4(c, base + s);
                 if (sub == 0 && rd * L + s < P.spp) {
-                    sum_c = sum_c + v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y,
-                                       v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);   // raytracer.cu:37-40
+                    sum_c = sum_c + clamp1(v);
                     sum_r = sum_r + v;
                 }
             }
@@ -1075,7 +1118,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
-        if (STATS && P.stats && lane == 0) {                  // profiling: heaviest group
+        if (CYC && P.stats && lane == 0) {                  // profiling: heaviest group
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
@@ -1086,10 +1129,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
             wave_sum += dur;
         }
-        ticket = resolve();
     }
     if (P.hist && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
-    if (STATS && P.stats && lane == 0) {
+    if (CYC && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
         if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
         if (wc.leaves) atomicAdd(&P.stats[2], wc.leaves);
@@ -1801,7 +1843,8 @@ bool opaque_scene(const rt_scene* s) {
 }
 
 int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y,
-                 bool want_stats, int occl_force = -1, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+                 bool want_stats, int occl_force = -1, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                 bool prof = false) {
     TraceParams P{};
     const rt::Scene& h = s->h;
     P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
@@ -1814,7 +1857,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.compact = o.compact; P.spp = o.spp; P.depth = h.depth;
     P.spp_off = s->d_spp;
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
-    P.stats = want_stats ? s->d_stats : nullptr; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
+    P.stats = (want_stats || prof) ? s->d_stats : nullptr; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
     if (o.textures) {
         int r;
         if ((r = ensure_atlas(s)) != RT_OK) return r;
@@ -1831,6 +1874,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     P.scramble = ticket_scramble((P.n_groups + NQ - 1) / NQ);
+    P.scramble_small = (unsigned long long)((P.n_groups + NQ - 1) / NQ + TPC) * (unsigned long long)P.scramble < (1ull << 32);
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * (NQ + 1) * sizeof(int), st));
@@ -1873,6 +1917,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
     if (tex) {
         fn = textured[use_lds ? 1 : 0][mode];
+    } else if (ft && park && S.tri_ax && prof && ns == 2) {
+        fn = (const void*)trace_kernel<2, true, M_PARK | M_FT | M_AXIS | M_PROF>;
     } else if (ft && park && S.tri_ax) {
         constexpr int PA = M_PARK | M_FT | M_AXIS;
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, PA> : ns <= 2 ? (const void*)trace_kernel<2, true, PA>
@@ -2372,7 +2418,8 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
 int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_t* counters) {
     CHECK_FINISHED(s);
     int r;
-    if (which == 4 || which == 5) {                           // full frame, counted kernel; 4: occlusion exit on
+    if (which == 4 || which == 5 || which == 6) {             // full frame: counted kernel (4: occlusion exit on),
+                                                              // 6: the fast kernel's profiling variant (M_PROF)
         if ((r = upload(s)) != RT_OK) return r;
         HIPCHK(hipSetDevice(s->device));
         if ((r = ensure_spp(s, spp)) != RT_OK) return r;
@@ -2384,7 +2431,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), s->stream));
             HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), s->stream));
             HIPCHK(hipEventRecord(s->ev[0], s->stream));
-            if ((r = launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0)) != RT_OK) return r;
+            if ((r = (which == 6 ? launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, false, -1, nullptr, nullptr, true)
+                                 : launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0))) != RT_OK)
+                return r;
             HIPCHK(hipEventRecord(s->ev[1], s->stream));
             HIPCHK(hipEventSynchronize(s->ev[1]));
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
