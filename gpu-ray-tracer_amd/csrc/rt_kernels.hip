@@ -271,7 +271,7 @@ __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv,
 // the same bits it would compute itself; only the origin chain is per leaf.
 // `inv` (axis-plane triangles, axis_plane_t): fl(1/mrd_a), NaN where |mrd_a| < 1e-5.
 struct DirPre { V3 mrd, inv; float scale, dir_len; };
-__device__ __forceinline__ float axis_inv(float d) { return fabsf(d) < THRESH ? __builtin_nanf("") : 1.0f / d; }
+__device__ __forceinline__ float axis_inv(float d) { return fabsf(d) < THRESH ? __builtin_nanf("") : rcp_cr(d); }
 template <bool AXIS = false>
 __device__ __forceinline__ DirPre dir_pre(V3 d) {
     DirPre p;
@@ -1444,6 +1444,8 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
             oi[i] = bx[6] != 0 && box_hit_f(L3(bx), L3(bx + 3), r, ray_inv(r));
             break;
         }
+        case 16: of[i] = rcp_cr(a[i]); break;                   // device CR reciprocal (rt_math.h)
+        case 17: of[i] = sqrt_cr(a[i]); break;                  // device CR sqrt
         case 15: {   // packed child-pair box test (pair_hit): two boxes (mn, mx, nd) x 2 vs one ray
             const float* bx = a + 14 * i;
             float q[12];
@@ -2495,12 +2497,13 @@ int rt_kat_device(const char* op, int n, const float* in0, const float* in1, con
                   uint64_t* ou) {
     static const char* ops[] = {"normalize3", "cross", "reflect", "refract", "quat_rotate", "quat_inverse", "quat_mul",
                                 "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow", "tri_hit_f", "box_hit_f",
-                                "box_pair"};
+                                "box_pair", "rcp_cr", "sqrt_cr"};
     // per-op sizes (floats): in0, in1, in2, out_f, out_i, out_u per element
     static const int sz[][6] = {{3, 0, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 2, 3, 1, 0},
                                 {4, 3, 0, 3, 0, 0}, {4, 0, 0, 4, 0, 0}, {4, 4, 0, 4, 0, 0}, {9, 6, 0, 3, 1, 0},
                                 {6, 0, 0, 6, 0, 0}, {3, 0, 0, 0, 0, 1}, {4, 0, 0, 9, 0, 0}, {7, 6, 0, 0, 1, 0},
-                                {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}, {14, 6, 0, 0, 2, 0}};
+                                {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}, {14, 6, 0, 0, 2, 0},
+                                {1, 0, 0, 1, 0, 0}, {1, 0, 0, 1, 0, 0}};
     if (!op || n <= 0) return fail(RT_ERR_ARG, "bad arguments");
     int k = -1;
     for (int i = 0; i < (int)(sizeof ops / sizeof *ops); i++) if (!strcmp(op, ops[i])) k = i;

@@ -159,3 +159,30 @@ def test_packed_pair_box_test_equals_exact(gpu, oracle):
     assert np.array_equal(out[:, 0], ref0)
     assert np.array_equal(out[:, 1], ref1)
     assert 0.2 < ref0.mean() < 0.9
+
+
+def test_device_cr_rcp_sqrt(gpu):
+    """rt_math.h rcp_cr/sqrt_cr (the device's short correctly rounded reciprocal and sqrt)
+    against IEEE float32 (numpy), bit for bit: every significand of the binades [1, 4)
+    (rounding depends only on the significand, and for sqrt on the exponent's parity),
+    both signs for rcp, plus 4M random bit patterns over the whole float range (the
+    out-of-range inputs take the compiler's general sequences)."""
+    sig = (np.arange(1 << 24, dtype=np.uint32) + np.uint32(0x3F800000)).view(np.float32)   # [1, 4)
+    rng = np.random.default_rng(5)
+    rnd = rng.integers(0, 1 << 32, size=1 << 22, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    edges = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 2.0 ** -125, 2.0 ** 125, 2.0 ** -126, 2.0 ** 126,
+                      2.0 ** -100, 2.0 ** 100, 1e-45, 3.4e38], np.float32)
+    with np.errstate(all="ignore"):
+        for x in (sig, -sig, rnd, edges):
+            x = np.ascontiguousarray(x.reshape(-1, 1))
+            got = gpu.kat_device("rcp_cr", x).reshape(-1)
+            ref = (np.float32(1.0) / x).reshape(-1)
+            nan = np.isnan(ref)
+            assert np.array_equal(np.isnan(got), nan)
+            assert np.array_equal(_bits(got[~nan]), _bits(ref[~nan])), "rcp_cr"
+            xs = np.abs(x)
+            got = gpu.kat_device("sqrt_cr", xs).reshape(-1)
+            ref = np.sqrt(xs).reshape(-1)
+            nan = np.isnan(ref)
+            assert np.array_equal(np.isnan(got), nan)
+            assert np.array_equal(_bits(got[~nan]), _bits(ref[~nan])), "sqrt_cr"
