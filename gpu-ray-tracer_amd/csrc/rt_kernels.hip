@@ -166,6 +166,10 @@ struct BvhRefs {
 #define RT_TPC 2             // work indices claimed per ticket (trace_kernel's group loop)
 #endif
 constexpr int TPC = RT_TPC;
+#ifndef RT_ZERO_AXIS_CUT
+#define RT_ZERO_AXIS_CUT 1   // 0: A/B variant, zero-direction axes unconstrained as in the reference (closest_hit)
+#endif
+constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
 #ifndef RT_PK_PAIR
 #define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
                              //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
@@ -467,8 +471,27 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         return hit;
     }
     const int n = S.n_leaf;
-    const RayInv ri = ray_inv(r);
+    RayInv ri = ray_inv(r);
     im = ri.exact ? INFINITY : fmaxf(fabsf(ri.ix), fmaxf(fabsf(ri.iy), fabsf(ri.iz)));
+    if (FT && ZERO_AXIS_CUT && S.prune_abs >= 0.0f) {
+        // Zero direction components (box bound, see above).  The reference's slab test
+        // skips an axis with d_a == 0 (bounding_box.cu:62-104), so such a ray "hits" every
+        // box its other coordinates cross, whatever o_a: the shadow rays of the directional
+        // light (0, -1, 1) and the primary rays of the centre column/row sweep whole rows
+        // of leaves.  Along the ray the coordinate stays o_a exactly (world and local:
+        // d_a and the local direction's component are 0), so an accepted hit lies within
+        // the slack of the leaf box on that axis: a node whose a-range excludes o_a by more
+        // than prune_abs has no acceptable hit below it (node boxes contain their leaves').
+        // The slab then becomes [K (mn - o - M), K (mx - o + M)] through the same fma and
+        // bias as a nonzero axis (pair_hit_at): both ends > 0 or < 0 exactly when o_a is
+        // outside [mn - M, mx + M] (a certain miss), else lo_a <= 0 < 1e-5 <= hi_a never
+        // binds (every nonzero axis bounds t by ~1e3; lo <= 0 is below any acceptable
+        // time, so entry bounds stay valid).  `im` keeps the nonzero axes only.
+        constexpr float K = 0x1p32f;
+        if (r.d.x == 0.0f) { ri.ix = K; ri.bx = K * S.prune_abs; }
+        if (r.d.y == 0.0f) { ri.iy = K; ri.by = K * S.prune_abs; }
+        if (r.d.z == 0.0f) { ri.iz = K; ri.bz = K * S.prune_abs; }
+    }
     if (FT) {
         // Ordered LBVH (fast kernel, S.ftree): same leaves and leaf order as the heap, so
         // each lane meets exactly the leaves its ray hits, in the heap's DFS order (a
@@ -677,6 +700,7 @@ struct TraceParams {
     int atlas_w, atlas_h;
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
+    unsigned* gdur;           // profiling (rt_profile_groups): per-group duration, 100 MHz ticks; NULL normally
 };
 
 // Textured mode (build-defined; phong.cu:18-23 leaves texture mapping a TODO): the
@@ -1127,6 +1151,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             const bool heavy = dur > thr;
             P.hf_next[g] = heavy ? 1 : 0;
             if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
+            if (P.gdur) P.gdur[g] = (unsigned)dur;
             wave_sum += dur;
         }
     }
@@ -1846,8 +1871,9 @@ bool opaque_scene(const rt_scene* s) {
 
 int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t* rgba, int* dbg, int dbg_x, int dbg_y,
                  bool want_stats, int occl_force = -1, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
-                 bool prof = false) {
+                 bool prof = false, unsigned* gdur = nullptr, int* geo = nullptr) {
     TraceParams P{};
+    P.gdur = gdur;
     const rt::Scene& h = s->h;
     P.cam = h.d_cam; P.dist_atten = h.dist_atten; P.ambience = h.ambience;
     P.W = h.cam.W; P.H = h.cam.H; P.row0 = o.row0; P.row_step = o.row_step;
@@ -1875,6 +1901,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.gw = gw; P.gh = P.px_per_wave / gw;
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
+    if (geo) { geo[0] = P.n_groups; geo[1] = P.gw; geo[2] = P.gh; geo[3] = P.n_gx; }
     P.scramble = ticket_scramble((P.n_groups + NQ - 1) / NQ);
     P.scramble_small = (unsigned long long)((P.n_groups + NQ - 1) / NQ + TPC) * (unsigned long long)P.scramble < (1ull << 32);
     P.work = s->d_work;
@@ -2491,6 +2518,51 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
     (void)hipFree(out);
     return RT_OK;
+}
+
+// Profiling aid (tools/group_profile.py, not on the product path): per-group durations
+// (100 MHz ticks) of the fast frame kernel over rows row0, row0 + row_step, ... (compact),
+// as bench.py's rank row0 of row_step renders them.  `reps` frames, each with the per-frame
+// BVH rebuild; the last one (scheduled from the previous frame's history) is recorded.
+// geo = {n_groups, gw, gh, n_gx}; *ms = the last frame's kernel time.
+int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, uint32_t* out, int64_t cap, int* geo,
+                      double* ms) {
+    CHECK_FINISHED(s);
+    if (!out || !geo || cap <= 0 || reps < 1 || row_step < 1 || row0 < 0) return fail(RT_ERR_ARG, "bad arguments");
+    int r;
+    if ((r = upload(s)) != RT_OK) return r;
+    HIPCHK(hipSetDevice(s->device));
+    if ((r = ensure_spp(s, spp)) != RT_OK) return r;
+    const int rows = (s->h.cam.H - row0 + row_step - 1) / row_step;
+    if (rows <= 0) return fail(RT_ERR_ARG, "no rows in the slice");
+    rt_render_opts o; rt_render_opts_default(&o);
+    o.spp = spp; o.row0 = row0; o.row_step = row_step; o.compact = 1;
+    uint32_t* d_rgba = nullptr;
+    unsigned* d_g = nullptr;
+    HIPCHK(hipMalloc((void**)&d_rgba, (size_t)s->h.cam.W * rows * sizeof(uint32_t)));
+    geo[0] = geo[1] = geo[2] = geo[3] = 0;
+    reps = std::max(reps, 2);                                 // frame 0 sizes the buffer and seeds the history
+    for (int i = 0; i < reps && r == RT_OK; i++) {
+        const bool rec = i == reps - 1;
+        if (rec) {
+            if (geo[0] <= 0 || geo[0] > cap) { r = fail(RT_ERR_LIMIT, "group buffer too small"); break; }
+            HIPCHK(hipMalloc((void**)&d_g, (size_t)geo[0] * sizeof(unsigned)));
+            HIPCHK(hipMemsetAsync(d_g, 0, (size_t)geo[0] * sizeof(unsigned), s->stream));
+        }
+        if ((r = build_bvh(s, s->stream)) != RT_OK) break;
+        r = launch_trace(s, o, s->stream, d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], false,
+                         rec ? d_g : nullptr, geo);
+    }
+    if (r == RT_OK) {
+        HIPCHK(hipEventSynchronize(s->ev[1]));
+        float t = 0;
+        HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
+        if (ms) *ms = t;
+        HIPCHK(hipMemcpy(out, d_g, (size_t)geo[0] * sizeof(unsigned), hipMemcpyDeviceToHost));
+    }
+    (void)hipFree(d_rgba);
+    (void)hipFree(d_g);
+    return r;
 }
 
 int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2, float* of, int32_t* oi,
