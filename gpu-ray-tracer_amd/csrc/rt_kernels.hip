@@ -1101,6 +1101,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
+        const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
         for (int rd = 0; rd < rounds; rd++) {
             const int k = rd * L + sub;
             const bool act = valid && k < P.spp;
@@ -1151,7 +1152,14 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             const bool heavy = dur > thr;
             P.hf_next[g] = heavy ? 1 : 0;
             if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
-            if (P.gdur) P.gdur[g] = (unsigned)dur;
+            if (P.gdur) {
+                P.gdur[g] = (unsigned)dur;
+                if (PROF) {                                    // wave step counts of the group
+                    unsigned* c = P.gdur + P.n_groups + 4 * (size_t)g;
+                    c[0] = (unsigned)(wc.wq - g_q0); c[1] = (unsigned)(wc.wpair - g_p0);
+                    c[2] = (unsigned)(wc.wleaf - g_l0); c[3] = (unsigned)(wc.wtri - g_r0);
+                }
+            }
             wave_sum += dur;
         }
     }
@@ -2524,9 +2532,11 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
 // (100 MHz ticks) of the fast frame kernel over rows row0, row0 + row_step, ... (compact),
 // as bench.py's rank row0 of row_step renders them.  `reps` frames, each with the per-frame
 // BVH rebuild; the last one (scheduled from the previous frame's history) is recorded.
-// geo = {n_groups, gw, gh, n_gx}; *ms = the last frame's kernel time.
-int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, uint32_t* out, int64_t cap, int* geo,
-                      double* ms) {
+// geo = {n_groups, gw, gh, n_gx}; *ms = the last frame's kernel time.  prof = 1: the recorded
+// frame runs the PROF variant (when the scene has one) and out[n_groups + 4 g ..] holds group
+// g's wave queries, child-pair steps, leaf visits and triangle iterations.
+int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, int prof, uint32_t* out, int64_t cap,
+                      int* geo, double* ms) {
     CHECK_FINISHED(s);
     if (!out || !geo || cap <= 0 || reps < 1 || row_step < 1 || row0 < 0) return fail(RT_ERR_ARG, "bad arguments");
     int r;
@@ -2542,15 +2552,16 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, ui
     HIPCHK(hipMalloc((void**)&d_rgba, (size_t)s->h.cam.W * rows * sizeof(uint32_t)));
     geo[0] = geo[1] = geo[2] = geo[3] = 0;
     reps = std::max(reps, 2);                                 // frame 0 sizes the buffer and seeds the history
+    const int nw = prof ? 5 : 1;                              // prof: + 4 wave step counts per group (PROF kernel)
     for (int i = 0; i < reps && r == RT_OK; i++) {
         const bool rec = i == reps - 1;
         if (rec) {
-            if (geo[0] <= 0 || geo[0] > cap) { r = fail(RT_ERR_LIMIT, "group buffer too small"); break; }
-            HIPCHK(hipMalloc((void**)&d_g, (size_t)geo[0] * sizeof(unsigned)));
-            HIPCHK(hipMemsetAsync(d_g, 0, (size_t)geo[0] * sizeof(unsigned), s->stream));
+            if (geo[0] <= 0 || (int64_t)geo[0] * nw > cap) { r = fail(RT_ERR_LIMIT, "group buffer too small"); break; }
+            HIPCHK(hipMalloc((void**)&d_g, (size_t)geo[0] * nw * sizeof(unsigned)));
+            HIPCHK(hipMemsetAsync(d_g, 0, (size_t)geo[0] * nw * sizeof(unsigned), s->stream));
         }
         if ((r = build_bvh(s, s->stream)) != RT_OK) break;
-        r = launch_trace(s, o, s->stream, d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], false,
+        r = launch_trace(s, o, s->stream, d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], rec && prof,
                          rec ? d_g : nullptr, geo);
     }
     if (r == RT_OK) {
@@ -2558,7 +2569,7 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, ui
         float t = 0;
         HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (ms) *ms = t;
-        HIPCHK(hipMemcpy(out, d_g, (size_t)geo[0] * sizeof(unsigned), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(out, d_g, (size_t)geo[0] * nw * sizeof(unsigned), hipMemcpyDeviceToHost));
     }
     (void)hipFree(d_rgba);
     (void)hipFree(d_g);

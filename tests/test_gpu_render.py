@@ -178,6 +178,25 @@ def test_fast_kernel_exact_grazing_rays(gpu):
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
 
 
+def test_fast_kernel_exact_zero_direction_axes(gpu):
+    """Zero-direction-axis cut (closest_hit): rays with d_x == 0 (centre column, sample 0)
+    and d_y == 0 (centre row) from origins on and around cube face planes, offset by
+    fractions and multiples of the pruning slack (~1.4e-3 here), so leaves whose slab is
+    skipped by the reference sit just inside and just outside the cut.  Every shadow ray
+    of world8_stress's directional light (0, -1, 1) has d_x == 0 as well."""
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    e = 0.4995
+    for off in (0.0, 1e-6, -1e-6, 7e-4, -7e-4, 1.4e-3, -1.4e-3, 3e-3, -3e-3):
+        for pos in ([e + off, 3 + e + off, -8.0], [-2 - e + off, 6 - e - off, -7.5]):
+            s.set_camera(pos, [0.0, 0.0, 0.0, 1.0])
+            fast = s.render(spp=2, want=want, stats=False)
+            full = s.render(spp=2, want=want, stats=True)
+            for k in want:
+                assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, k)
+            assert (full["hit_inst"] >= 0).mean() > 0.05, pos          # (a centre row may run in a gap)
+
+
 def test_fast_kernel_exact_random_cameras(gpu):
     """Fast kernel (ordered LBVH, pruning, axis-plane triangle path with its shared-plane
     skip and in-plane reject) == counted reference-heap kernel, bit for bit, from seeded
