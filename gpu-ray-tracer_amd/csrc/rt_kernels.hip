@@ -1933,7 +1933,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     s->hctl_zeroed = -1;
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
-    const bool ft = !tex && mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
+    const bool ft = mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
     const size_t lds = lds_bytes(S, ft);
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
@@ -1952,7 +1952,11 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
     const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    if (tex) {
+    if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
+        constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
+        fn = S.tri_ax ? (ns <= 2 ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<NG, true, TA>)
+                      : (ns <= 2 ? (const void*)trace_kernel<2, true, TF> : (const void*)trace_kernel<NG, true, TF>);
+    } else if (tex) {
         fn = textured[use_lds ? 1 : 0][mode];
     } else if (ft && park && S.tri_ax && prof && ns == 2) {
         fn = (const void*)trace_kernel<2, true, M_PARK | M_FT | M_AXIS | M_PROF>;
