@@ -1102,6 +1102,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
+        const unsigned long long g_c0 = wc.cyc_q, g_c1 = wc.cyc_leaf, g_c2 = wc.cyc_sample, g_c3 = wc.cyc_post;
+        const unsigned long long g_m0 = CYC ? __builtin_amdgcn_s_memtime() : 0;
         for (int rd = 0; rd < rounds; rd++) {
             const int k = rd * L + sub;
             const bool act = valid && k < P.spp;
@@ -1143,7 +1145,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
         }
-        if (CYC && P.stats && lane == 0) {                  // profiling: heaviest group
+        if (STATS && P.stats && lane == 0) {                 // profiling: heaviest group (PROF: rt_profile_groups)
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
@@ -1154,10 +1156,13 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
             if (P.gdur) {
                 P.gdur[g] = (unsigned)dur;
-                if (PROF) {                                    // wave step counts of the group
-                    unsigned* c = P.gdur + P.n_groups + 4 * (size_t)g;
+                if (PROF) {                                    // wave step counts and cycle split of the group
+                    unsigned* c = P.gdur + P.n_groups + 9 * (size_t)g;
                     c[0] = (unsigned)(wc.wq - g_q0); c[1] = (unsigned)(wc.wpair - g_p0);
                     c[2] = (unsigned)(wc.wleaf - g_l0); c[3] = (unsigned)(wc.wtri - g_r0);
+                    c[4] = (unsigned)(wc.cyc_q - g_c0); c[5] = (unsigned)(wc.cyc_leaf - g_c1);
+                    c[6] = (unsigned)(wc.cyc_sample - g_c2); c[7] = (unsigned)(wc.cyc_post - g_c3);
+                    c[8] = (unsigned)(__builtin_amdgcn_s_memtime() - g_m0);
                 }
             }
             wave_sum += dur;
@@ -2537,8 +2542,9 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
 // as bench.py's rank row0 of row_step renders them.  `reps` frames, each with the per-frame
 // BVH rebuild; the last one (scheduled from the previous frame's history) is recorded.
 // geo = {n_groups, gw, gh, n_gx}; *ms = the last frame's kernel time.  prof = 1: the recorded
-// frame runs the PROF variant (when the scene has one) and out[n_groups + 4 g ..] holds group
-// g's wave queries, child-pair steps, leaf visits and triangle iterations.
+// frame runs the PROF variant (when the scene has one) and out[n_groups + 9 g ..] holds group
+// g's wave queries, child-pair steps, leaf visits, triangle iterations, then shader cycles in
+// queries, in leaf visits, in trace_sample, after queries (state machine), and in the group.
 int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, int prof, uint32_t* out, int64_t cap,
                       int* geo, double* ms) {
     CHECK_FINISHED(s);
@@ -2556,7 +2562,7 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, in
     HIPCHK(hipMalloc((void**)&d_rgba, (size_t)s->h.cam.W * rows * sizeof(uint32_t)));
     geo[0] = geo[1] = geo[2] = geo[3] = 0;
     reps = std::max(reps, 2);                                 // frame 0 sizes the buffer and seeds the history
-    const int nw = prof ? 5 : 1;                              // prof: + 4 wave step counts per group (PROF kernel)
+    const int nw = prof ? 10 : 1;                             // prof: + 9 counters per group (PROF kernel)
     for (int i = 0; i < reps && r == RT_OK; i++) {
         const bool rec = i == reps - 1;
         if (rec) {
