@@ -97,6 +97,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
+    int n_mats, n_tris, n_meshes;   // record counts (LDS shading cache, M_SHADE)
     int ident_all;            // every instance and mesh rotation is the identity (cube worlds)
     float prune_abs;          // distance-pruning slack M0 (< 0: pruning off), see closest_hit
     const TriAx* tri_ax;      // axis-plane triangle records (fast kernel; null unless ident_all)
@@ -157,6 +158,13 @@ struct BvhRefs {
     const float4* pair;     // [3n]
     const int* leaf;        // [n]  instance of leaf node n+i (bvh.cu ordering[])
     const float4* inst;     // [n_inst] (px, py, pz, mesh | 0x80000000 if the pose is not identity)
+    // shading-side records (materials, lights, triangles, meshes): the scene's arrays, or
+    // their LDS copies in M_SHADE kernels (hit normal, lighting and frame transitions read
+    // them per lane after every query)
+    const DMat* mats;
+    const DLight* lights;
+    const DTri* tris;
+    const DMesh* meshes;
 };
 
 #ifndef RT_FILTERED
@@ -166,6 +174,9 @@ struct BvhRefs {
 #define RT_TPC 2             // work indices claimed per ticket (trace_kernel's group loop)
 #endif
 constexpr int TPC = RT_TPC;
+#ifndef RT_SHADE_LDS
+#define RT_SHADE_LDS 1       // materials, lights, triangles and meshes copied into LDS (M_SHADE kernels)
+#endif
 #ifndef RT_ZERO_AXIS_CUT
 #define RT_ZERO_AXIS_CUT 1   // 0: A/B variant, zero-direction axes unconstrained as in the reference (closest_hit)
 #endif
@@ -397,8 +408,8 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
 __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, const Best& b, int& mat) {
     int mesh_id;
     const Pose ip = inst_pose(S, bv, b.inst, mesh_id);
-    const Pose mp = S.meshes[mesh_id].pose;
-    const DTri& T = S.tris[b.tri];
+    const Pose mp = bv.meshes[mesh_id].pose;
+    const DTri& T = bv.tris[b.tri];
     mat = T.mat;
     float b0 = 1.0f - b.u - b.v;
     V3 n = normalized((b0 * T.n0 + b.u * T.n1) + b.v * T.n2);
@@ -709,9 +720,9 @@ struct TraceParams {
 // index (point sampling, clamp addressing: the reference's texture setup); other hits
 // keep the material's Kd.  gfx950 has no image/sampler instructions (HIP marks tex2D
 // unavailable there), so the atlas is a plain float4 array in HBM.
-__device__ __forceinline__ V4 hit_kd(const TraceParams& P, const SceneView& S, const Best& b, int mat) {
-    const DTri& T = S.tris[b.tri];
-    if (!T.tex) return S.mats[mat].Kd;
+__device__ __forceinline__ V4 hit_kd(const TraceParams& P, const BvhRefs& bv, const Best& b, int mat) {
+    const DTri& T = bv.tris[b.tri];
+    if (!T.tex) return bv.mats[mat].Kd;
     const float x = (T.tx + b.u * T.ux) + b.v * T.vx;
     const float y = (T.ty + b.u * T.uy) + b.v * T.vy;
     const int ix = (int)fminf(fmaxf(x, 0.0f), (float)(P.atlas_w - 1));
@@ -793,7 +804,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         while (st == ST_ADVANCE || st == ST_LIGHT) {
             if (st == ST_LIGHT) {
                 if (li < S.n_lights) {
-                    const DLight L = S.lights[li];
+                    const DLight L = bv.lights[li];
                     const V3 hpos = at(cur.ray, is_time);          // org_ray.at(isect.time) (phong.cu:48)
                     Ray to;
                     if (L.type == 0) {                             // PointLight::shine (light.cu:63-70)
@@ -828,7 +839,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 st = ST_WAIT_NORMAL;
                 continue;
             }
-            const DMat& m = S.mats[is_mat];
+            const DMat& m = bv.mats[is_mat];
             bool do_pop = false;
             if (cur.type == F_REFLECT) {                           // scene.cu:129-148 (frame's own hit)
                 cur.type = F_REFRACT;
@@ -846,8 +857,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 dbg(P, me, 3);
                 cur.type = F_NORMAL;
                 float n1, n2;
-                if (cur.in_obj) { n1 = S.mats[cur.last_mat].eta; n2 = 1.0f; }
-                else { n1 = 1.0f; n2 = S.mats[cur.last_mat].eta; }
+                if (cur.in_obj) { n1 = bv.mats[cur.last_mat].eta; n2 = 1.0f; }
+                else { n1 = 1.0f; n2 = bv.mats[cur.last_mat].eta; }
                 V3 hp, nn;
                 if (fl & 4) { hp = stk[top].hit_pt; nn = stk[top].norm; }
                 else { hp = at(cur.ray, is_time); nn = is_norm; }
@@ -918,11 +929,11 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 continue;
             }
             is_time = b.time; is_norm = hn; is_mat = hmat;
-            if (TEX) is_kd = hit_kd(P, S, b, hmat);
+            if (TEX) is_kd = hit_kd(P, bv, b, hmat);
             fl &= ~4;                                              // hit point / normal = at(ray, is_time), is_norm
             if (cur.depth > 0) {                                   // scene.cu:109-121
                 if (cur.in_obj) {
-                    const V4 kt = S.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
+                    const V4 kt = bv.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
                     cur.atten = cur.atten * v4(pow_fast(is_time, kt.x), pow_fast(is_time, kt.y),
                                                pow_fast(is_time, kt.z), pow_fast(is_time, kt.w));
                 }
@@ -931,7 +942,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             } else {
                 fl |= 2;                                           // popped after illumination (frame still needed)
             }
-            const DMat& m = S.mats[is_mat];                        // org_light (phong.cu:36-39)
+            const DMat& m = bv.mats[is_mat];                       // org_light (phong.cu:36-39)
             summed = m.Ke + m.Ka * P.ambience;
             li = 0;
             st = ST_LIGHT;
@@ -941,7 +952,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
         bool light_done = true;
         V4 att = rv;
         if (hit && !(b.time > max_t)) {
-            const DMat& m = S.mats[hmat];
+            const DMat& m = bv.mats[hmat];
             if (!m.refractive) {
                 att = v4(0, 0, 0, 0);
             } else {
@@ -956,8 +967,8 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
             }
         }
         if (light_done) {
-            const V4 inc = (S.lights[li].type == 0) ? da * att : att;   // PointLight: dist_atten * attenuate()
-            const DMat& mm = S.mats[is_mat];
+            const V4 inc = (bv.lights[li].type == 0) ? da * att : att;  // PointLight: dist_atten * attenuate()
+            const DMat& mm = bv.mats[is_mat];
             summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
             li++;
             st = ST_LIGHT;
@@ -967,17 +978,41 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
 }
 
 // stage_bvh's LDS image size (16-B multiple)
-__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false) {
-    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst;
-    return ((48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf + 15) & ~(size_t)15) + ((16 * (size_t)S.n_inst + 15) & ~(size_t)15);
+__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~(size_t)15; }
+// LDS shading cache (M_SHADE): mats | lights | tris | meshes, each 16-B aligned
+__host__ __device__ inline size_t shade_bytes(const SceneView& S) {
+    return a16(sizeof(DMat) * (size_t)S.n_mats) + a16(sizeof(DLight) * (size_t)S.n_lights) +
+           a16(sizeof(DTri) * (size_t)S.n_tris) + a16(sizeof(DMesh) * (size_t)S.n_meshes);
+}
+__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false) {
+    const size_t sh = shade ? shade_bytes(S) : 0;
+    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
+    return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
+}
+// word copy of n records of T into LDS at `dst` (block-cooperative)
+template <class T> __device__ __forceinline__ const T* stage_words(unsigned char* dst, const T* src, int n) {
+    static_assert(sizeof(T) % 4 == 0 && alignof(T) <= 16, "word-granular records");
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+    const int w = (int)(sizeof(T) / 4) * n;
+    for (int i = threadIdx.x; i < w; i += blockDim.x) d32[i] = s32[i];
+    return reinterpret_cast<const T*>(dst);
 }
 
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
-template <bool LDS, bool FT = false>
+template <bool LDS, bool FT = false, bool SHADE = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
     bv.fnode = S.fnode; bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    bv.mats = S.mats; bv.lights = S.lights; bv.tris = S.tris; bv.meshes = S.meshes;
+    if (LDS && SHADE) {                                    // after the BVH image (lds_bytes without the cache)
+        unsigned char* p = smem + lds_bytes(S, FT);
+        bv.mats = stage_words(p, S.mats, S.n_mats);       p += a16(sizeof(DMat) * (size_t)S.n_mats);
+        bv.lights = stage_words(p, S.lights, S.n_lights); p += a16(sizeof(DLight) * (size_t)S.n_lights);
+        bv.tris = stage_words(p, S.tris, S.n_tris);       p += a16(sizeof(DTri) * (size_t)S.n_tris);
+        bv.meshes = stage_words(p, S.meshes, S.n_meshes);
+    }
     if (LDS && FT) {                                       // ordered LBVH | inst4
         const int nf = 4 * (S.n_real - 1);
         float4* fn = reinterpret_cast<float4*>(smem);
@@ -1020,19 +1055,20 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
 // MODE bit 6 (PROF): profiling variant of the fast kernel -- wave-level step counts and
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64;
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
-    const BvhRefs bv = stage_bvh<LDS, FT>(S, smem);
+    constexpr bool SHADE = (MODE & M_SHADE) != 0;
+    const BvhRefs bv = stage_bvh<LDS, FT, SHADE>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
-    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT)) + threadIdx.x : nullptr;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
@@ -1855,6 +1891,7 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     v.ftree = (!RT_NO_FTREE && s->n_real >= 2 && s->fdepth <= FT_MAX_DEPTH) ? 1 : 0; v.inst4 = s->d_inst4;
     v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
+    v.n_mats = (int)s->h.d_mats.size(); v.n_tris = (int)s->h.d_tris.size(); v.n_meshes = (int)s->h.d_meshes.size();
     v.ident_all = 1;
     for (const auto& i : s->h.d_insts) v.ident_all &= i.pose.identity ? 1 : 0;
     for (const auto& m : s->h.d_meshes) v.ident_all &= m.pose.identity ? 1 : 0;
@@ -1957,6 +1994,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
     const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
+    // LDS shading cache beside the parked main kernel (not with the profiling variant)
+    const bool shade = RT_SHADE_LDS && park && ft && S.tri_ax && !prof &&
+                       lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
     if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
         constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
         fn = S.tri_ax ? (ns <= 2 ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<NG, true, TA>)
@@ -1965,6 +2005,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         fn = textured[use_lds ? 1 : 0][mode];
     } else if (ft && park && S.tri_ax && prof && ns == 2) {
         fn = (const void*)trace_kernel<2, true, M_PARK | M_FT | M_AXIS | M_PROF>;
+    } else if (ft && park && S.tri_ax && shade) {
+        constexpr int PS = M_PARK | M_FT | M_AXIS | M_SHADE;
+        fn = ns <= 0 ? (const void*)trace_kernel<0, true, PS> : ns <= 2 ? (const void*)trace_kernel<2, true, PS>
+                                                                 : (const void*)trace_kernel<NG, true, PS>;
     } else if (ft && park && S.tri_ax) {
         constexpr int PA = M_PARK | M_FT | M_AXIS;
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, PA> : ns <= 2 ? (const void*)trace_kernel<2, true, PA>
@@ -1981,7 +2025,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = park ? lds + park_bytes : use_lds ? lds : 0;
+    const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
