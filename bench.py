@@ -7,10 +7,13 @@ Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit que
 
 One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
 rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
-the packed RGBA8 rows to rank 0 and the row un-permute.  Over RCCL the gather of
-frame k runs on the collective stream while frame k+1 renders (double-buffered
-slices); the timed region ends after the last frame's gather and un-permute.  The frame stays in HBM
-(the PCIe read-back is reported separately as `ms_per_step_with_readback`).
+the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined two deep
+(rtamd.dist.FramePipeline, rt_scene_set_frame_slots): frame k+1 renders on a second
+stream and starts on the CUs that frame k's longest pixel groups leave idle, and frame
+k's gather runs on the collective stream meanwhile.  The timed region ends after the last
+frame's gather and un-permute.  `frame_latency_ms` is one frame issued alone and waited
+for; `--no-overlap` times serial frames.  The frame stays in HBM (the PCIe read-back is
+reported separately as `ms_per_step_with_readback`).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 the driver
 uses torch.distributed.run (one process per GPU, RCCL over xGMI).
@@ -50,6 +53,7 @@ def parse():
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
+    p.add_argument("--no-overlap", action="store_true", help="serial frames (no two-deep frame pipeline)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -115,20 +119,31 @@ def main():
         scene.load_atlas()
     W, H = scene.width, scene.height
     my_rows = len(rtdist.rows_of(rank, world, H))
-    # RCCL: double-buffered slices, frame k's gather overlaps frame k+1's render (rtamd.dist)
-    fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo, slots=2)
-    part = fb.part
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
     frame_no = [0]
+    overlap = not args.no_overlap and not gloo
+    if overlap:                           # two frames in flight (rtamd.dist.FramePipeline)
+        scene.set_frame_slots(2)
+        fb = rtdist.FramePipeline(W, H, world, rank, "cuda", dist)
+        part = fb.parts[0]
+    else:                                 # serial frames; RCCL gather of frame k overlaps frame k+1
+        fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo, slots=2)
+        part = fb.part
+
+    def render(buf, st, timing):
+        scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
+                            compact=True, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream,
+                            timing=timing, textures=args.textures)
 
     def step(timing):
         k = frame_no[0]
         frame_no[0] += 1
-        scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
-                            compact=True, rgba_ptr=fb.slot_part(k).data_ptr(), stream=stream.cuda_stream,
-                            timing=timing, textures=args.textures)
-        fb.gather(k)
+        if overlap:
+            fb.step(k, lambda buf, st: render(buf, st, timing))
+        else:
+            render(fb.slot_part(k), stream, timing)
+            fb.gather(k)
 
     # per-frame work counters (deterministic): one untimed counted render of this rank's rows
     st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
@@ -157,6 +172,18 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     tm = scene.timing_collect()
+    # latency of one frame issued alone (render + gather + un-permute, waited for)
+    lat = []
+    for _ in range(max(3, args.steps // 2)):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        step(False)
+        fb.finish()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t3)
+    lat_ms = sorted(lat)[len(lat) // 2] * 1e3
     # read-back variant (reference post-condition: framebuffer host readable)
     t2 = time.perf_counter()
     host = None
@@ -209,7 +236,7 @@ def main():
                    "parallelism": ("row-cyclic x%d + %s gather" % (world, "gloo host-staged" if gloo else "RCCL"))
                                   if world > 1 else "single GPU"},
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
-        "cold_frame_ms": round(cold_ms, 4),
+        "cold_frame_ms": round(cold_ms, 4), "frame_latency_ms": round(lat_ms, 4), "frame_overlap": overlap,
         "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),
         "tri_tests_per_frame": int(tris), "trace_kernel_ms": round(trace_ms, 4), "bvh_build_ms": round(bvh_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

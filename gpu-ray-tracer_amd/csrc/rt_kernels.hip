@@ -1584,8 +1584,36 @@ struct rt_scene {
     int n_leaf = 0;
     bool uploaded = false, bvh_valid = false;
     std::vector<uint32_t> canvas;    // host framebuffer (Canvas buffer, canvas.cu:7)
+    // Frame slots (rt_scene_set_frame_slots): with 2 slots, consecutive frames alternate
+    // between two copies of the per-frame state (BVH, work counters, scheduling history),
+    // so a frame on another stream can start on CUs freed by the previous frame's tail.
+    // The fields above always hold the current slot; `other` holds the idle one (swap_slot).
+    struct Slot {
+        Box* d_tree = nullptr; float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_fnode = nullptr;
+        int* d_work = nullptr; bool work_zeroed = false, bvh_valid = false;
+        int* d_hlist[2] = {nullptr, nullptr}; unsigned char* d_hflag[2] = {nullptr, nullptr};
+        unsigned long long* d_hctl = nullptr;
+        int hist_cap = 0, hist_parity = 0, hctl_zeroed = -1;
+        long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    } other;
+    int n_slots = 1, cur_slot = 0;
+    hipEvent_t slot_done[2] = {nullptr, nullptr};   // last frame of each slot (recorded on its stream)
+    bool slot_pending[2] = {false, false};
     ~rt_scene();
 };
+
+// Exchange the current per-frame state with the idle slot's.
+void swap_slot(rt_scene* s) {
+    rt_scene::Slot& o = s->other;
+    std::swap(s->d_tree, o.d_tree); std::swap(s->d_node_pair, o.d_node_pair); std::swap(s->d_leaf, o.d_leaf);
+    std::swap(s->d_fnode, o.d_fnode); std::swap(s->d_work, o.d_work);
+    std::swap(s->work_zeroed, o.work_zeroed); std::swap(s->bvh_valid, o.bvh_valid);
+    for (int p = 0; p < 2; p++) { std::swap(s->d_hlist[p], o.d_hlist[p]); std::swap(s->d_hflag[p], o.d_hflag[p]); }
+    std::swap(s->d_hctl, o.d_hctl); std::swap(s->hist_cap, o.hist_cap); std::swap(s->hist_parity, o.hist_parity);
+    std::swap(s->hctl_zeroed, o.hctl_zeroed);
+    for (int i = 0; i < 8; i++) std::swap(s->hist_key[i], o.hist_key[i]);
+    s->cur_slot ^= 1;
+}
 
 namespace {
 thread_local std::string g_err;
@@ -1604,6 +1632,7 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
 }
 
 int upload_inst4(rt_scene* s);
+int ensure_other_slot(rt_scene* s);
 
 // TriAx records (rt_math.h) of the axis-plane triangle path: axis, plane coordinate,
 // shared-plane flag and the in-plane reject box with its host-checked error bound.
@@ -1766,6 +1795,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
+    if (s->n_slots == 2) return ensure_other_slot(s);
     return RT_OK;
 }
 
@@ -1780,6 +1810,21 @@ int upload_inst4(rt_scene* s) {
         v[i] = make_float4(d.pose.p.x, d.pose.p.y, d.pose.p.z, fw);
     }
     if (!v.empty()) HIPCHK(hipMemcpy(s->d_inst4, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+// Buffers of the idle frame slot (sizes as in upload) and the slot events.
+int ensure_other_slot(rt_scene* s) {
+    rt_scene::Slot& o = s->other;
+    if (o.d_work) return RT_OK;
+    const size_t nl = std::max(1, s->n_leaf);
+    HIPCHK(hipMalloc((void**)&o.d_node_pair, 3 * nl * sizeof(float4)));
+    HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
+    HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
+    HIPCHK(hipMalloc((void**)&o.d_work, 16 * (NQ + 1) * sizeof(int)));
+    for (auto& e : s->slot_done) if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    o.work_zeroed = false; o.bvh_valid = false;
     return RT_OK;
 }
 
@@ -2050,7 +2095,7 @@ rt::Material mat_from(const float* m) {
     return r;
 }
 
-void invalidate(rt_scene* s) { s->bvh_valid = false; }
+void invalidate(rt_scene* s) { s->bvh_valid = false; s->other.bvh_valid = false; }
 
 }  // namespace
 
@@ -2066,6 +2111,10 @@ rt_scene::~rt_scene() {
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : tev) (void)hipEventDestroy(e);
+    dfree(other.d_tree); dfree(other.d_node_pair); dfree(other.d_leaf); dfree(other.d_fnode); dfree(other.d_work);
+    for (int p = 0; p < 2; p++) { dfree(other.d_hlist[p]); dfree(other.d_hflag[p]); }
+    dfree(other.d_hctl);
+    for (auto& e : slot_done) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -2381,6 +2430,11 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         te = &s->tev[s->tev_used];
         s->tev_used += 4;
     }
+    if (s->n_slots == 2) {                                   // alternate frame slots (rt_scene_set_frame_slots)
+        if ((r = ensure_other_slot(s)) != RT_OK) return r;
+        swap_slot(s);
+        if (s->slot_pending[s->cur_slot]) HIPCHK(hipStreamWaitEvent(st, s->slot_done[s->cur_slot], 0));
+    }
     if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st, te ? te[0] : nullptr, te ? te[1] : nullptr)) != RT_OK) {
@@ -2413,6 +2467,10 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         return r;
     }
     if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
+    if (s->n_slots == 2) {                                   // the slot is free again once this frame is done
+        HIPCHK(hipEventRecord(s->slot_done[s->cur_slot], st));
+        s->slot_pending[s->cur_slot] = true;
+    }
     if (o->sync || timed || o->host_outputs) HIPCHK(hipStreamSynchronize(st));
     if (o->host_outputs) {
         if (o->rgba) HIPCHK(hipMemcpy(o->rgba, oo.rgba, out_px * 4, hipMemcpyDeviceToHost));
@@ -2430,6 +2488,16 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         stats->bvh_ms = a; stats->trace_ms = b;
     }
     return RT_OK;
+}
+
+int rt_scene_set_frame_slots(rt_scene* s, int n) {
+    CHECK_FINISHED(s);
+    if (n != 1 && n != 2) return fail(RT_ERR_ARG, "frame slots: 1 or 2");
+    if (n == s->n_slots) return RT_OK;
+    if (s->uploaded) { HIPCHK(hipSetDevice(s->device)); HIPCHK(hipDeviceSynchronize()); }   // nothing in flight
+    s->slot_pending[0] = s->slot_pending[1] = false;
+    s->n_slots = n;
+    return (n == 2 && s->uploaded) ? ensure_other_slot(s) : RT_OK;
 }
 
 int rt_timing_collect(rt_scene* s, double* bvh_ms, double* trace_ms, int* n) {

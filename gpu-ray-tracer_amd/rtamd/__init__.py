@@ -35,7 +35,7 @@ SYMBOLS = [
     "rt_render_opts_default", "rt_render", "rt_update_scene", "rt_canvas_read", "rt_canvas_host_ptr",
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
-    "rt_scene_atlas_info",
+    "rt_scene_atlas_info", "rt_scene_set_frame_slots",
 ]
 
 
@@ -115,6 +115,7 @@ def lib():
     L.rt_set_device.argtypes = [ip]
     L.rt_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ip)]
     L.rt_device_count.argtypes = [ctypes.POINTER(ip)]
+    L.rt_scene_set_frame_slots.argtypes = [vp, ip]
     _lib = L
     return L
 
@@ -358,6 +359,11 @@ class Scene:
         st = Stats()
         _check(lib().rt_render(self._h, ctypes.byref(o), ctypes.byref(st) if stats else None))
         return st.as_dict() if stats else None
+
+    def set_frame_slots(self, n):
+        """1 (default) or 2: consecutive frames alternate between two copies of the per-frame
+        state, so frames on different streams overlap (rt_scene_set_frame_slots)."""
+        _check(lib().rt_scene_set_frame_slots(self._h, int(n)))
 
     def timing_collect(self):
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()

@@ -65,3 +65,13 @@ def test_cpp_shim_and_cli_compile_against_the_abi(tmp_path):
         r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, src, "-o", str(tmp_path / "a.out"),
                             "-L", libdir, "-lrt_amd"], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
+
+
+def test_frame_slots_arguments(rt):
+    """rt_scene_set_frame_slots takes 1 or 2 (host-side state; no GPU needed)."""
+    s = rt.Scene.load_json(scene_path("world1"), 16, 16)
+    s.set_frame_slots(2)
+    s.set_frame_slots(1)
+    with pytest.raises(rt.RtError) as e:
+        s.set_frame_slots(3)
+    assert e.value.code == rt.RT_ERR_ARG
