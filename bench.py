@@ -7,10 +7,10 @@ Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit que
 
 One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
 rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
-the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined two deep
-(rtamd.dist.FramePipeline, rt_scene_set_frame_slots): frame k+1 renders on a second
-stream and starts on the CUs that frame k's longest pixel groups leave idle, and frame
-k's gather runs on the collective stream meanwhile.  The timed region ends after the last
+the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined four deep
+(rtamd.dist.FramePipeline, rt_scene_set_frame_slots): frame k+1 renders on another
+stream and starts on the CUs that the previous frames' longest pixel groups leave idle,
+and frame k's gather runs on the collective stream meanwhile.  The timed region ends after the last
 frame's gather and un-permute.  `frame_latency_ms` is one frame issued alone and waited
 for; `--no-overlap` times serial frames.  The frame stays in HBM (the PCIe read-back is
 reported separately as `ms_per_step_with_readback`).
@@ -24,6 +24,12 @@ import os
 import sys
 import time
 
+# Frames in flight run on their own streams; HIP maps streams round-robin onto
+# GPU_MAX_HW_QUEUES hardware queues (4 by default), and streams sharing a queue serialise.
+# Main + 4 render streams + the collective's stream need more than 4 (measured: three
+# frames in flight 1.49 ms/frame on 4 queues, 1.41 on 8).
+# (HIP's default, also the pool's box setting, is 4; RT_BENCH_HW_QUEUES overrides the 8 used here.)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
 import torch  # first: the HIP runtime torch loads is the one librt_amd.so binds to
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -53,7 +59,8 @@ def parse():
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
-    p.add_argument("--no-overlap", action="store_true", help="serial frames (no two-deep frame pipeline)")
+    p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
+    p.add_argument("--frames-in-flight", type=int, default=4, help="frame pipeline depth (1-4)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -122,10 +129,11 @@ def main():
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
     frame_no = [0]
-    overlap = not args.no_overlap and not gloo
-    if overlap:                           # two frames in flight (rtamd.dist.FramePipeline)
-        scene.set_frame_slots(2)
-        fb = rtdist.FramePipeline(W, H, world, rank, "cuda", dist)
+    depth = max(1, min(4, args.frames_in_flight))
+    overlap = not args.no_overlap and not gloo and depth > 1
+    if overlap:                           # frames in flight (rtamd.dist.FramePipeline)
+        scene.set_frame_slots(depth)
+        fb = rtdist.FramePipeline(W, H, world, rank, "cuda", dist, depth=depth)
         part = fb.parts[0]
     else:                                 # serial frames; RCCL gather of frame k overlaps frame k+1
         fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo, slots=2)
@@ -164,7 +172,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(not args.no_kernel_timing)
+        step(not args.no_kernel_timing and not overlap)
     fb.finish()                                             # the last frame's gather + un-permute
     torch.cuda.synchronize()
     if dist:
@@ -172,18 +180,22 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     tm = scene.timing_collect()
-    # latency of one frame issued alone (render + gather + un-permute, waited for)
+    # latency of one frame issued alone (render + gather + un-permute, waited for); with frames
+    # in flight the kernels' event-timed durations come from these lone frames (a launch that
+    # overlaps other frames' kernels is longer than its cost)
     lat = []
     for _ in range(max(3, args.steps // 2)):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t3 = time.perf_counter()
-        step(False)
+        step(overlap and not args.no_kernel_timing)
         fb.finish()
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t3)
     lat_ms = sorted(lat)[len(lat) // 2] * 1e3
+    if overlap:
+        tm = scene.timing_collect()
     # read-back variant (reference post-condition: framebuffer host readable)
     t2 = time.perf_counter()
     host = None
@@ -236,7 +248,7 @@ def main():
                    "parallelism": ("row-cyclic x%d + %s gather" % (world, "gloo host-staged" if gloo else "RCCL"))
                                   if world > 1 else "single GPU"},
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
-        "cold_frame_ms": round(cold_ms, 4), "frame_latency_ms": round(lat_ms, 4), "frame_overlap": overlap,
+        "cold_frame_ms": round(cold_ms, 4), "frame_latency_ms": round(lat_ms, 4), "frames_in_flight": depth if overlap else 1,
         "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),
         "tri_tests_per_frame": int(tris), "trace_kernel_ms": round(trace_ms, 4), "bvh_build_ms": round(bvh_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1584,10 +1584,11 @@ struct rt_scene {
     int n_leaf = 0;
     bool uploaded = false, bvh_valid = false;
     std::vector<uint32_t> canvas;    // host framebuffer (Canvas buffer, canvas.cu:7)
-    // Frame slots (rt_scene_set_frame_slots): with 2 slots, consecutive frames alternate
-    // between two copies of the per-frame state (BVH, work counters, scheduling history),
-    // so a frame on another stream can start on CUs freed by the previous frame's tail.
-    // The fields above always hold the current slot; `other` holds the idle one (swap_slot).
+    // Frame slots (rt_scene_set_frame_slots): with n > 1 slots, consecutive frames rotate
+    // through n copies of the per-frame state (BVH, work counters, scheduling history), so a
+    // frame on another stream can start on CUs freed by the previous frames' tails.  The
+    // fields above always hold the current slot; store[i] the others (store[cur] is stale).
+    static constexpr int MAX_SLOTS = 4;
     struct Slot {
         Box* d_tree = nullptr; float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_fnode = nullptr;
         int* d_work = nullptr; bool work_zeroed = false, bvh_valid = false;
@@ -1595,24 +1596,29 @@ struct rt_scene {
         unsigned long long* d_hctl = nullptr;
         int hist_cap = 0, hist_parity = 0, hctl_zeroed = -1;
         long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-    } other;
+    } store[MAX_SLOTS];
     int n_slots = 1, cur_slot = 0;
-    hipEvent_t slot_done[2] = {nullptr, nullptr};   // last frame of each slot (recorded on its stream)
-    bool slot_pending[2] = {false, false};
+    hipEvent_t slot_done[MAX_SLOTS] = {};            // last frame of each slot (recorded on its stream)
+    bool slot_pending[MAX_SLOTS] = {};
     ~rt_scene();
 };
 
-// Exchange the current per-frame state with the idle slot's.
-void swap_slot(rt_scene* s) {
-    rt_scene::Slot& o = s->other;
-    std::swap(s->d_tree, o.d_tree); std::swap(s->d_node_pair, o.d_node_pair); std::swap(s->d_leaf, o.d_leaf);
-    std::swap(s->d_fnode, o.d_fnode); std::swap(s->d_work, o.d_work);
-    std::swap(s->work_zeroed, o.work_zeroed); std::swap(s->bvh_valid, o.bvh_valid);
-    for (int p = 0; p < 2; p++) { std::swap(s->d_hlist[p], o.d_hlist[p]); std::swap(s->d_hflag[p], o.d_hflag[p]); }
-    std::swap(s->d_hctl, o.d_hctl); std::swap(s->hist_cap, o.hist_cap); std::swap(s->hist_parity, o.hist_parity);
-    std::swap(s->hctl_zeroed, o.hctl_zeroed);
-    for (int i = 0; i < 8; i++) std::swap(s->hist_key[i], o.hist_key[i]);
-    s->cur_slot ^= 1;
+// Move the current per-frame state into store[cur_slot] and load slot i's.
+void select_slot(rt_scene* s, int i) {
+    if (i == s->cur_slot) return;
+    auto xfer = [](auto& a, auto& b) { a = b; };
+    auto move = [&](rt_scene::Slot& o, bool save) {
+        auto f = [&](auto& field, auto& slot) { if (save) xfer(slot, field); else xfer(field, slot); };
+        f(s->d_tree, o.d_tree); f(s->d_node_pair, o.d_node_pair); f(s->d_leaf, o.d_leaf); f(s->d_fnode, o.d_fnode);
+        f(s->d_work, o.d_work); f(s->work_zeroed, o.work_zeroed); f(s->bvh_valid, o.bvh_valid);
+        for (int p = 0; p < 2; p++) { f(s->d_hlist[p], o.d_hlist[p]); f(s->d_hflag[p], o.d_hflag[p]); }
+        f(s->d_hctl, o.d_hctl); f(s->hist_cap, o.hist_cap); f(s->hist_parity, o.hist_parity);
+        f(s->hctl_zeroed, o.hctl_zeroed);
+        for (int k = 0; k < 8; k++) f(s->hist_key[k], o.hist_key[k]);
+    };
+    move(s->store[s->cur_slot], true);
+    move(s->store[i], false);
+    s->cur_slot = i;
 }
 
 namespace {
@@ -1753,6 +1759,14 @@ void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
 void free_atlas(rt_scene* s);
 int ensure_atlas(rt_scene* s);
 
+// The scene's own stream, created on first use: a caller passing its own streams (frame
+// pipelining) keeps every HIP stream of the process on a hardware queue of its own
+// (GPU_MAX_HW_QUEUES = 4; streams beyond that share queues and serialise).
+hipStream_t sstream(rt_scene* s) {
+    if (!s->stream) (void)hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    return s->stream;
+}
+
 int upload(rt_scene* s) {
     if (s->uploaded) return RT_OK;
     int ndev = 0;
@@ -1763,7 +1777,6 @@ int upload(rt_scene* s) {
     HIPCHK(hipGetDeviceProperties(&prop, s->device));
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         return fail(RT_ERR_NODEV, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
-    HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     for (auto& e : s->ev) HIPCHK(hipEventCreate(&e));
     const rt::Scene& h = s->h;
     auto up = [&](auto*& dst, const auto& vec) -> int {
@@ -1795,7 +1808,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     s->uploaded = true;
-    if (s->n_slots == 2) return ensure_other_slot(s);
+    if (s->n_slots > 1) return ensure_other_slot(s);
     return RT_OK;
 }
 
@@ -1813,18 +1826,20 @@ int upload_inst4(rt_scene* s) {
     return RT_OK;
 }
 
-// Buffers of the idle frame slot (sizes as in upload) and the slot events.
+// Buffers of the frame slots other than the current one (sizes as in upload), slot events.
 int ensure_other_slot(rt_scene* s) {
-    rt_scene::Slot& o = s->other;
-    if (o.d_work) return RT_OK;
     const size_t nl = std::max(1, s->n_leaf);
-    HIPCHK(hipMalloc((void**)&o.d_node_pair, 3 * nl * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
-    HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
-    HIPCHK(hipMalloc((void**)&o.d_work, 16 * (NQ + 1) * sizeof(int)));
-    for (auto& e : s->slot_done) if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    o.work_zeroed = false; o.bvh_valid = false;
+    for (int i = 0; i < s->n_slots; i++) {
+        rt_scene::Slot& o = s->store[i];
+        if (i == s->cur_slot || o.d_work) continue;
+        HIPCHK(hipMalloc((void**)&o.d_node_pair, 3 * nl * sizeof(float4)));
+        HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
+        HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
+        HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
+        HIPCHK(hipMalloc((void**)&o.d_work, 16 * (NQ + 1) * sizeof(int)));
+        o.work_zeroed = false; o.bvh_valid = false;
+    }
+    for (int i = 0; i < s->n_slots; i++) if (!s->slot_done[i]) HIPCHK(hipEventCreateWithFlags(&s->slot_done[i], hipEventDisableTiming));
     return RT_OK;
 }
 
@@ -2095,7 +2110,10 @@ rt::Material mat_from(const float* m) {
     return r;
 }
 
-void invalidate(rt_scene* s) { s->bvh_valid = false; s->other.bvh_valid = false; }
+void invalidate(rt_scene* s) {
+    s->bvh_valid = false;
+    for (auto& o : s->store) o.bvh_valid = false;
+}
 
 }  // namespace
 
@@ -2111,9 +2129,13 @@ rt_scene::~rt_scene() {
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : tev) (void)hipEventDestroy(e);
-    dfree(other.d_tree); dfree(other.d_node_pair); dfree(other.d_leaf); dfree(other.d_fnode); dfree(other.d_work);
-    for (int p = 0; p < 2; p++) { dfree(other.d_hlist[p]); dfree(other.d_hflag[p]); }
-    dfree(other.d_hctl);
+    for (int i = 0; i < MAX_SLOTS; i++) {                      // store[cur_slot] is the (freed) current state
+        if (i == cur_slot) continue;
+        Slot& o = store[i];
+        dfree(o.d_tree); dfree(o.d_node_pair); dfree(o.d_leaf); dfree(o.d_fnode); dfree(o.d_work);
+        for (int p = 0; p < 2; p++) { dfree(o.d_hlist[p]); dfree(o.d_hflag[p]); }
+        dfree(o.d_hctl);
+    }
     for (auto& e : slot_done) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
@@ -2419,7 +2441,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     HIPCHK(hipSetDevice(s->device));
     if ((size_t)s->h.cam.W * s->h.cam.H > (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame larger than 2^31 pixels");
     if ((r = ensure_spp(s, o->spp)) != RT_OK) return r;
-    hipStream_t st = o->stream ? (hipStream_t)o->stream : s->stream;
+    hipStream_t st = o->stream ? (hipStream_t)o->stream : sstream(s);
     const bool timed = stats != nullptr;
     hipEvent_t* te = nullptr;
     if (o->timing) {
@@ -2430,9 +2452,9 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         te = &s->tev[s->tev_used];
         s->tev_used += 4;
     }
-    if (s->n_slots == 2) {                                   // alternate frame slots (rt_scene_set_frame_slots)
+    if (s->n_slots > 1) {                                    // rotate frame slots (rt_scene_set_frame_slots)
         if ((r = ensure_other_slot(s)) != RT_OK) return r;
-        swap_slot(s);
+        select_slot(s, (s->cur_slot + 1) % s->n_slots);
         if (s->slot_pending[s->cur_slot]) HIPCHK(hipStreamWaitEvent(st, s->slot_done[s->cur_slot], 0));
     }
     if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
@@ -2467,7 +2489,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         return r;
     }
     if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
-    if (s->n_slots == 2) {                                   // the slot is free again once this frame is done
+    if (s->n_slots > 1) {                                    // the slot is free again once this frame is done
         HIPCHK(hipEventRecord(s->slot_done[s->cur_slot], st));
         s->slot_pending[s->cur_slot] = true;
     }
@@ -2492,12 +2514,13 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
 
 int rt_scene_set_frame_slots(rt_scene* s, int n) {
     CHECK_FINISHED(s);
-    if (n != 1 && n != 2) return fail(RT_ERR_ARG, "frame slots: 1 or 2");
+    if (n < 1 || n > rt_scene::MAX_SLOTS) return fail(RT_ERR_ARG, "frame slots: 1 to 4");
     if (n == s->n_slots) return RT_OK;
     if (s->uploaded) { HIPCHK(hipSetDevice(s->device)); HIPCHK(hipDeviceSynchronize()); }   // nothing in flight
-    s->slot_pending[0] = s->slot_pending[1] = false;
+    select_slot(s, 0);
+    for (auto& p : s->slot_pending) p = false;
     s->n_slots = n;
-    return (n == 2 && s->uploaded) ? ensure_other_slot(s) : RT_OK;
+    return (n > 1 && s->uploaded) ? ensure_other_slot(s) : RT_OK;
 }
 
 int rt_timing_collect(rt_scene* s, double* bvh_ms, double* trace_ms, int* n) {
@@ -2551,14 +2574,14 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, 1)) != RT_OK) return r;
-    if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
-    HIPCHK(hipMemsetAsync(s->d_dbg, 0, 4096 * sizeof(int), s->stream));
+    if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
+    HIPCHK(hipMemsetAsync(s->d_dbg, 0, 4096 * sizeof(int), sstream(s)));
     rt_render_opts o;
     rt_render_opts_default(&o);
     o.row0 = y; o.row_step = s->h.cam.H;                                  // just the row of (x, y)
-    if ((r = launch_trace(s, o, s->stream, s->d_canvas, s->d_dbg, x, y, true)) != RT_OK) return r;
+    if ((r = launch_trace(s, o, sstream(s), s->d_canvas, s->d_dbg, x, y, true)) != RT_OK) return r;
     std::vector<int> log(4096);
-    HIPCHK(hipStreamSynchronize(s->stream));
+    HIPCHK(hipStreamSynchronize(sstream(s)));
     HIPCHK(hipMemcpy(log.data(), s->d_dbg, log.size() * sizeof(int), hipMemcpyDeviceToHost));
     static const char* names[] = {"", "shooting a ray", "preparing to shoot a reflection ray",
                                   "preparing to shoot a refraction ray", "shooting shadow ray"};
@@ -2582,17 +2605,17 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         HIPCHK(hipSetDevice(s->device));
         if ((r = ensure_spp(s, spp)) != RT_OK) return r;
         rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
-        if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+        if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
-            HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), s->stream));
-            HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), s->stream));
-            HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), s->stream));
-            HIPCHK(hipEventRecord(s->ev[0], s->stream));
-            if ((r = (which == 6 ? launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, false, -1, nullptr, nullptr, true)
-                                 : launch_trace(s, o, s->stream, s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0))) != RT_OK)
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), sstream(s)));
+            HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), sstream(s)));
+            HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), sstream(s)));
+            HIPCHK(hipEventRecord(s->ev[0], sstream(s)));
+            if ((r = (which == 6 ? launch_trace(s, o, sstream(s), s->d_canvas, nullptr, -1, -1, false, -1, nullptr, nullptr, true)
+                                 : launch_trace(s, o, sstream(s), s->d_canvas, nullptr, -1, -1, true, which == 4 ? 1 : 0))) != RT_OK)
                 return r;
-            HIPCHK(hipEventRecord(s->ev[1], s->stream));
+            HIPCHK(hipEventRecord(s->ev[1], sstream(s)));
             HIPCHK(hipEventSynchronize(s->ev[1]));
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
@@ -2606,7 +2629,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, spp)) != RT_OK) return r;
-    if ((r = build_bvh(s, s->stream)) != RT_OK) return r;
+    if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
     s->work_zeroed = false;                                  // the primary kernels reset d_work themselves
     rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
     TraceParams P{};
@@ -2631,12 +2654,12 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     HIPCHK(hipMalloc((void**)&out, (size_t)P.W * P.H * P.lanes_per_px * sizeof(float4)));
     float total = 0;
     for (int i = 0; i < reps; i++) {
-        HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), s->stream));
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), s->stream));
-        HIPCHK(hipEventRecord(s->ev[0], s->stream));
+        HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), sstream(s)));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), sstream(s)));
+        HIPCHK(hipEventRecord(s->ev[0], sstream(s)));
         void* args[] = {&P, &S, &out};
-        HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, s->stream));
-        HIPCHK(hipEventRecord(s->ev[1], s->stream));
+        HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, sstream(s)));
+        HIPCHK(hipEventRecord(s->ev[1], sstream(s)));
         HIPCHK(hipEventSynchronize(s->ev[1]));
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
@@ -2680,10 +2703,10 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, in
         if (rec) {
             if (geo[0] <= 0 || (int64_t)geo[0] * nw > cap) { r = fail(RT_ERR_LIMIT, "group buffer too small"); break; }
             HIPCHK(hipMalloc((void**)&d_g, (size_t)geo[0] * nw * sizeof(unsigned)));
-            HIPCHK(hipMemsetAsync(d_g, 0, (size_t)geo[0] * nw * sizeof(unsigned), s->stream));
+            HIPCHK(hipMemsetAsync(d_g, 0, (size_t)geo[0] * nw * sizeof(unsigned), sstream(s)));
         }
-        if ((r = build_bvh(s, s->stream)) != RT_OK) break;
-        r = launch_trace(s, o, s->stream, d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], rec && prof,
+        if ((r = build_bvh(s, sstream(s))) != RT_OK) break;
+        r = launch_trace(s, o, sstream(s), d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], rec && prof,
                          rec ? d_g : nullptr, geo);
     }
     if (r == RT_OK) {

@@ -98,36 +98,37 @@ class RowCyclicFrame:
 
 
 class FramePipeline:
-    """Two frames in flight (bench.py over RCCL, or one GPU): frame k renders on stream
-    k % 2 into slice buffer k % 2, with the scene in two frame slots
-    (rt_scene_set_frame_slots), so frame k+1's blocks start on the CUs that frame k's
-    longest groups leave idle.  The RGBA8 slices of frame k are gathered asynchronously
-    into gather buffer k % 2 on rank 0; frame k's un-permute runs on the main stream once
-    frame k+1 has been issued.  Every wait is a stream dependency:
-      - frame k's render waits for frame k-2's gather (it rewrites that slice buffer);
-      - frame k's gather waits for frame k-2's un-permute (it rewrites that gather buffer);
+    """`depth` frames in flight (bench.py over RCCL, or one GPU): frame k renders on stream
+    k % depth into slice buffer k % depth, with the scene in `depth` frame slots
+    (rt_scene_set_frame_slots), so frame k+1's blocks start on the CUs that the previous
+    frames' longest groups leave idle.  The RGBA8 slices of frame k are gathered
+    asynchronously into gather buffer k % depth on rank 0; frame k's un-permute runs on the
+    main stream once frame k+1 has been issued.  Every wait is a stream dependency:
+      - frame k's render waits for frame k-depth's gather (it rewrites that slice buffer);
+      - frame k's gather waits for frame k-depth's un-permute (same gather buffer);
       - frame k's un-permute waits for frame k's gather.
     Images are the ones serial frames give; only the overlap changes."""
 
-    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32):
+    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
+        self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
-        self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(2)]
-        self.streams = [torch.cuda.Stream(device=device) for _ in range(2)]
+        self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(D)]
+        self.streams = [torch.cuda.Stream(device=device) for _ in range(D)]
         self.main = torch.cuda.current_stream(device)
-        self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(2)]
+        self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(D)]
                       if (world > 1 and rank == 0) else None)
         self.out = torch.empty((height, width), dtype=dtype, device=device) if (world > 1 and rank == 0) else None
-        self.work = [None, None]        # gather of the frame last rendered in each slot
-        self.unperm = [None, None]      # event after the un-permute that last read each gather buffer
-        self.pending = [False, False]   # slot's frame gathered but not yet un-permuted
+        self.work = [None] * D          # gather of the frame last rendered in each slot
+        self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
+        self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
         self.last = -1
 
     @property
     def frame(self):
         """The last finished frame (rank 0; call finish() first)."""
         if self.world == 1:
-            return self.parts[self.last % 2] if self.last >= 0 else None
+            return self.parts[self.last % self.depth] if self.last >= 0 else None
         return self.out
 
     def _unpermute(self, s):
@@ -149,25 +150,25 @@ class FramePipeline:
 
     def step(self, k, render):
         """Issue frame k: render(part, stream) enqueues the render of this rank's rows."""
-        s = k % 2
+        s = k % self.depth
         st = self.streams[s]
         with torch.cuda.stream(st):
             if self.work[s] is not None:
-                self.work[s].wait()                     # frame k-2's gather has read parts[s]
+                self.work[s].wait()                     # frame k-depth's gather has read parts[s]
             render(self.parts[s], st)
             if self.world > 1:
                 if self.unperm[s] is not None:
-                    st.wait_event(self.unperm[s])       # frame k-2's un-permute has read gbufs[s]
+                    st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]
                 gl = list(self.gbufs[s].unbind(0)) if self.rank == 0 else None
                 self.work[s] = self.dist.gather(self.parts[s], gl, dst=0, async_op=True)
                 self.pending[s] = True
         if k >= 1:
-            self._unpermute((k - 1) % 2)
+            self._unpermute((k - 1) % self.depth)
         self.last = k
 
     def finish(self):
         """Complete every issued frame (stream-ordered on the main stream)."""
-        for s in (0, 1):
+        for s in range(self.depth):
             self._unpermute(s)
         for st in self.streams:
             self.main.wait_stream(st)

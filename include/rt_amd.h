@@ -137,12 +137,12 @@ typedef struct rt_stats {
 void rt_render_opts_default(rt_render_opts* o);
 int rt_render(rt_scene* s, const rt_render_opts* opts, rt_stats* stats);
 
-/* Frame slots (1 = default, or 2).  The reference rebuilds its BVH inside every
+/* Frame slots (1 = default, up to 4).  The reference rebuilds its BVH inside every
  * update_scene call (raytracer.cu:103-119), so a frame owns per-frame state: BVH, work
- * counters and scheduling history.  With 2 slots, consecutive rt_render calls alternate
- * between two copies of that state.  A frame issued on another stream then overlaps the
- * previous frame's tail on the CUs it has freed.  Each call waits (stream-ordered, no host
- * sync) for the last frame of its slot.  The caller gives frames in flight distinct
+ * counters and scheduling history.  With n slots, consecutive rt_render calls rotate
+ * through n copies of that state.  Frames issued on other streams then overlap the
+ * previous frames' tails on the CUs they have freed.  Each call waits (stream-ordered, no
+ * host sync) for the last frame of its slot.  The caller gives frames in flight distinct
  * outputs.  Images are identical either way.  Waits for the device when changed. */
 int rt_scene_set_frame_slots(rt_scene* s, int n_slots);
 

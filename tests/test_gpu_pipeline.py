@@ -1,5 +1,5 @@
-"""Two frames in flight (rt_scene_set_frame_slots + rtamd.dist.FramePipeline): frames
-issued on alternating streams, with the per-frame state in two slots, are the frames
+"""Frames in flight (rt_scene_set_frame_slots + rtamd.dist.FramePipeline): frames
+issued on rotating streams, with the per-frame state in 2-4 slots, are the frames
 serial rendering gives, bit for bit -- on one GPU, and for the row-cyclic split with its
 gather and un-permute (world 2, one process: the other rank's slice is supplied by a
 stand-in gather)."""
@@ -23,24 +23,24 @@ def _serial(gpu, scene, w, h, spp, row0=0, row_step=1):
     return buf
 
 
-@pytest.mark.parametrize("scene,spp", [("world8_stress", 4), ("world16", 1)])
-def test_frame_slots_two_streams_identical(gpu, scene, spp):
+@pytest.mark.parametrize("scene,spp,depth", [("world8_stress", 4, 2), ("world16", 1, 3), ("world8", 2, 4)])
+def test_frame_slots_streams_identical(gpu, scene, spp, depth):
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
     import rtamd.dist as rtdist
     w, h = 240, 160
     ref = _serial(gpu, scene, w, h, spp)
     s = gpu.Scene.load_json(scene_path(scene), w, h)
-    s.set_frame_slots(2)
-    pipe = rtdist.FramePipeline(w, h, 1, 0, "cuda")
-    for k in range(7):
+    s.set_frame_slots(depth)
+    pipe = rtdist.FramePipeline(w, h, 1, 0, "cuda", depth=depth)
+    for k in range(9):
         pipe.step(k, lambda buf, st: s.render_device(spp=spp, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream))
         if k % 3 == 2:
             torch.cuda.synchronize()
             assert torch.equal(pipe.finish(), ref), k
     torch.cuda.synchronize()
     assert torch.equal(pipe.finish(), ref)
-    assert torch.equal(pipe.parts[0], ref) and torch.equal(pipe.parts[1], ref)
+    assert all(torch.equal(p, ref) for p in pipe.parts)
 
 
 class _Work:
@@ -72,9 +72,9 @@ def test_pipeline_world2_gather_and_unpermute(gpu):
     other = torch.zeros((rtdist.slice_height(2, h), w), dtype=torch.int32, device="cuda")
     other[:r1.shape[0]] = r1
     s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
-    s.set_frame_slots(2)
-    pipe = rtdist.FramePipeline(w, h, 2, 0, "cuda", _TwoRankGather(other))
-    for k in range(5):
+    s.set_frame_slots(3)
+    pipe = rtdist.FramePipeline(w, h, 2, 0, "cuda", _TwoRankGather(other), depth=3)
+    for k in range(7):
         pipe.step(k, lambda buf, st: s.render_device(spp=spp, row0=0, row_step=2, compact=True,
                                                      rgba_ptr=buf.data_ptr(), stream=st.cuda_stream))
     torch.cuda.synchronize()

@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline $*"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-overlap $*"   # serial frames: one launch at a time, as bench.py times the kernel
 run() { local name=$1; shift; timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o "$name" -- python3 "$R/bench.py" $ARGS > "$OUT/$name.log" 2>&1; }
 run kt --kernel-trace --stats || { echo "kernel-trace run failed"; exit 1; }
 run fetch --kernel-trace --pmc FETCH_SIZE || { echo "pmc FETCH_SIZE failed"; exit 1; }
