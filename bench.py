@@ -39,6 +39,9 @@ import rtamd.dist as rtdist  # noqa: E402
 
 METRIC = "Mrays/sec (primary+secondary) + frame ms, 1080p world8_stress, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2400 MHz max clock, one wave64 VALU instruction per
+# SIMD every 2 cycles -> peak VALU issue in wave-instructions per second
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2
 B_NODE, B_LEAF = 28, 816        # SURVEY §8d algorithmic bytes: BoundingBox / leaf (pose+mesh+12 tris)
 
 
@@ -229,14 +232,15 @@ def main():
     bvh_ms = tm["bvh_ms_total"] / max(1, tm["frames"])
     algo_bytes = B_NODE * st["nodes"] + B_LEAF * st["leaves"] + 4 * W * my_rows
     achieved = algo_bytes / (trace_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, issue = None, {}
     if os.path.exists(args.pmc):
         try:
             pm = json.load(open(args.pmc))
             key = "%s_%dx%d_spp%d_n%d" % (args.scene, W, H, args.spp, world)
             traffic = pm.get(key, {}).get("hbm_bytes_per_launch")
+            issue = pm.get(key, {}).get("issue", {})
         except Exception:
-            traffic = None
+            traffic, issue = None, {}
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
@@ -257,6 +261,15 @@ def main():
                      "note": "algorithmic bytes = 28*nodes + 816*leaves + 4*W*rows (SURVEY 8d); scene is L2-resident, "
                              "so frac > 1 is possible"},
     }
+    if issue.get("SQ_INSTS_VALU"):
+        # what bounds the kernel in fact: VALU issue plus dependent latency.
+        # VALU wave-instructions per launch from the committed PMC profile, over this run's
+        # event-timed kernel duration
+        rate = issue["SQ_INSTS_VALU"] / (trace_ms * 1e-3)
+        out["issue_bound"] = {"bound": "valu_issue", "achieved": round(rate / 1e9, 2), "peak": VALU_ISSUE_PEAK / 1e9,
+                              "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4),
+                              "valu_insts_per_launch": int(issue["SQ_INSTS_VALU"]),
+                              "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU)"}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, scene_path)
     print(json.dumps(out), flush=True)

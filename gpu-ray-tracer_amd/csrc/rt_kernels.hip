@@ -1341,6 +1341,12 @@ __host__ __device__ inline void fnode_split(const unsigned long long* k, int nr,
     last = i < j ? j : i;
 }
 
+#ifdef RT_BUILD_STAMPS      // experiment builds only: phase timestamps of the BVH build
+__device__ unsigned long long g_build_stamps[16];
+#define BSTAMP(i) do { __syncthreads(); if (threadIdx.x == 0) g_build_stamps[i] = wall_clock64(); } while (0)
+#else
+#define BSTAMP(i) do {} while (0)
+#endif
 template <bool LDS_TREE>
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1351,6 +1357,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     else tree.t = A.tree;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n = A.n;
+    BSTAMP(0);
     for (int i = tid; i < A.n_work; i += nt) A.work[i] = 0;
     if (A.hctl && tid < 2) A.hctl[tid] = 0;
 
@@ -1367,10 +1374,74 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         idx[i] = i;
     }
     __syncthreads();
-    // bitonic sort on (key, index): identical order to a stable sort by key.  Strides >= 64
-    // exchange through the LDS; the strides below 64 of each merge run in registers within
-    // the wave (lane ^ stride), one LDS round trip and barrier per merge instead of per stride.
-    for (int size = 2; size <= n; size <<= 1) {
+    BSTAMP(1);
+    // Sort on (key, index): identical order to a stable sort by key (thrust sort_by_key,
+    // bvh.cu:86).  Entries [n_inst, n) are padding with key ~0 and the largest indices, so
+    // they already sit at their rank; only [0, n_inst) moves.
+    const int m = A.n_inst, nch = (m + 63) >> 6;
+    bool sorted = false;
+    if constexpr (LDS_TREE) {
+        if (n >= 64 && nch * 64 <= nt) {
+            // Chunked rank sort: wave w sorts entries [64w, 64w + 64) in registers (bitonic
+            // network over lanes), then each entry's rank = its lane + its rank in every other
+            // sorted chunk (branchless binary search in LDS).  Earlier chunks hold smaller
+            // indices, so equal keys count there (<=) and not in later chunks (<).  Three
+            // barriers instead of the bitonic network's 20 LDS phases.  The sorted chunks are
+            // staged in the tree's LDS region (8 * 64 * nch <= 8n < 28 (2n - 1) bytes).
+            unsigned long long* S = reinterpret_cast<unsigned long long*>(smem + 12 * (size_t)n);
+            const int lane = tid & 63, c = tid >> 6;
+            unsigned long long k = ~0ull;
+            int x = tid;
+            if (tid < nch * 64) {                                  // whole waves
+                if (tid < m) k = keys[tid];
+                for (int size = 2; size <= 64; size <<= 1) {
+                    const bool up = (lane & size) == 0;
+                    for (int st = size >> 1; st > 0; st >>= 1) {
+                        const unsigned lo = __shfl_xor((unsigned)k, st), hi = __shfl_xor((unsigned)(k >> 32), st);
+                        const unsigned long long pk = ((unsigned long long)hi << 32) | lo;
+                        const int px = __shfl_xor(x, st);
+                        const bool mine_less = k < pk || (k == pk && x < px);
+                        if (mine_less != (((lane & st) == 0) == up)) { k = pk; x = px; }
+                    }
+                }
+                S[tid] = k;
+            }
+            __syncthreads();
+            int pos = lane;
+            if (tid < m) {
+                for (int cb = 0; cb < nch; cb += 4) {              // four independent searches in flight
+                    int p4[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int sp = 32; sp >= 1; sp >>= 1) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            const int cc = cb + u;
+                            if (cc < nch && cc != c) {
+                                const unsigned long long v = S[(cc << 6) + p4[u] + sp - 1];
+                                if (cc < c ? v <= k : v < k) p4[u] += sp;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int cc = cb + u;
+                        if (cc < nch && cc != c) {
+                            const unsigned long long v = S[(cc << 6) + 63];
+                            pos += p4[u] + (p4[u] == 63 && (cc < c ? v <= k : v < k));
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid < m) { keys[pos] = k; idx[pos] = x; }
+            __syncthreads();
+            sorted = true;
+        }
+    }
+    // bitonic sort on (key, index) otherwise.  Strides >= 64 exchange through the LDS; the
+    // strides below 64 of each merge run in registers within the wave (lane ^ stride), one
+    // LDS round trip and barrier per merge instead of per stride.
+    for (int size = 2; size <= n && !sorted; size <<= 1) {
         int stride = size >> 1;
         for (; stride >= 64 || (n < 64 && stride > 0); stride >>= 1) {
             for (int i = tid; i < n; i += nt) {
@@ -1402,10 +1473,12 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             __syncthreads();
         }
     }
+    BSTAMP(2);
     // reorder (bvh.cu:34-41: the box is recomputed, same arithmetic) and pairwise level
     // merges (bvh.cu:43-61)
     for (int i = tid; i < n; i += nt) tree.put(i, inst_box(idx[i]));
     __syncthreads();
+    BSTAMP(3);
     {
         int lvl = 0, size = n, out = n;
         while (size >= 2) {
@@ -1414,6 +1487,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             lvl += size; out += size / 2; size >>= 1;
         }
     }
+    BSTAMP(4);
     // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
     for (int k = tid; k < 2 * n; k += nt) {
         Box b;
@@ -1428,6 +1502,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     // leaves.  Internal node i splits at the highest differing key bit; the child
     // whose leaves are later in storage order is child A (visited first), so
     // leaves are met in the heap's DFS order (heap leaf k <-> storage 2n-1-k).
+    BSTAMP(5);
     const int nr = A.n_real;                    // real leaves = storage [0, nr) (padding sorts last)
     for (int i = tid; i < nr - 1; i += nt) {
         int first, last, gamma;
@@ -1450,6 +1525,7 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         }
         refs[2] = refs[3] = 0;
     }
+    BSTAMP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -2511,6 +2587,14 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     }
     return RT_OK;
 }
+
+#ifdef RT_BUILD_STAMPS
+int rt_exp_build_stamps(unsigned long long* out) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), 16 * sizeof(unsigned long long)));
+    return RT_OK;
+}
+#endif
 
 int rt_scene_set_frame_slots(rt_scene* s, int n) {
     CHECK_FINISHED(s);

@@ -51,6 +51,8 @@ def main():
     write_kib, nw = per_dispatch(root, "WRITE_SIZE")
     rdreq, _ = per_dispatch(root, "TCC_EA0_RDREQ_sum")
     wrreq, _ = per_dispatch(root, "TCC_EA0_WRREQ_sum")
+    issue = {c: per_dispatch(root, c)[0] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                                                  "SQ_WAIT_ANY")}
     if fetch_kib is None or write_kib is None:
         sys.exit("no FETCH_SIZE/WRITE_SIZE rows for trace_kernel under " + root)
     frame_bytes = 4 * W * rows
@@ -63,6 +65,8 @@ def main():
                 "TCC_EA0_RDREQ": rdreq, "TCC_EA0_WRREQ": wrreq},
         "write_calibration": {"frame_store_bytes": frame_bytes, "write_over_frame": wr / frame_bytes},
         "kernel_trace": kernel_stats(root),
+        # wave-level instruction counts per launch (secondary bound: VALU issue, bench.py)
+        "issue": {k: v for k, v in issue.items() if v is not None},
         "source": os.path.relpath(root),
     }
     db = json.load(open(out)) if os.path.exists(out) else {}
