@@ -48,8 +48,8 @@ B_NODE, B_LEAF = 28, 816        # SURVEY §8d algorithmic bytes: BoundingBox / l
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--scene", default="world8_stress")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
