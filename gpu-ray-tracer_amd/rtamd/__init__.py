@@ -361,8 +361,9 @@ class Scene:
         return st.as_dict() if stats else None
 
     def set_frame_slots(self, n):
-        """1 (default) or 2: consecutive frames alternate between two copies of the per-frame
-        state, so frames on different streams overlap (rt_scene_set_frame_slots)."""
+        """1 (default) to 4: consecutive frames rotate through n copies of the per-frame
+        state (BVH, work counters, scheduling history), so frames issued on different streams
+        overlap (rt_scene_set_frame_slots)."""
         _check(lib().rt_scene_set_frame_slots(self._h, int(n)))
 
     def timing_collect(self):

@@ -9,11 +9,14 @@ GPUs; any torch.distributed backend works, the CPU tests use gloo) and the row
 un-permute there.  Slices are padded to ceil(H/G) rows so every message has the
 same size.
 
-Pipelining (`slots=2`, bench.py over RCCL): frame k renders into slice buffer k % 2
-and its gather is issued asynchronously, so it runs on the collective stream while
-frame k+1 renders; frame k's un-permute is enqueued when frame k+1's gather is issued
-(or by `finish()`), after waiting for frame k's gather.  The waits are stream
-dependencies, not host synchronisation.
+Pipelining, two forms:
+- `RowCyclicFrame(slots=2)` (serial frames, bench.py --no-overlap): frame k renders into
+  slice buffer k % 2 and its gather is issued asynchronously, so it runs on the collective
+  stream while frame k+1 renders; frame k's un-permute is enqueued when frame k+1's gather
+  is issued (or by `finish()`), after waiting for frame k's gather.
+- `FramePipeline(depth)` (bench.py default, depth 4): frames in flight on their own
+  streams, see the class.
+The waits are stream dependencies, not host synchronisation.
 """
 import torch
 
