@@ -2084,6 +2084,14 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     int gw = 1;
     if ((P.px_per_wave & (P.px_per_wave - 1)) == 0) { while (gw * gw < P.px_per_wave) gw <<= 1; }
     else gw = P.px_per_wave;
+    // Row slices with rows >= 8 frame rows apart (N >= 8 ranks): a 2-row group would pair
+    // rows that far apart, so groups are one row (8 x 1 at 8 spp).  Measured with four frames
+    // in flight: 8-way slice 0.234 -> 0.229 ms; whole frames and 2-way slices keep 4 x 2
+    // (8 x 1 there: +3.4% / +2%; profiles/r01/ab_group_shape_v31.log).
+    if (o.row_step >= 8) gw = P.px_per_wave;
+#ifdef RT_GROUP_W                                          // experiment builds: fixed group width
+    if (P.px_per_wave % RT_GROUP_W == 0) gw = RT_GROUP_W;
+#endif
     P.gw = gw; P.gh = P.px_per_wave / gw;
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);

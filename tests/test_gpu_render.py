@@ -81,14 +81,15 @@ def test_update_scene_postcondition(gpu, oracle):
     assert np.array_equal(s.canvas(), c)
 
 
-def test_row_slices_compose(gpu):
-    """Row-cyclic slices (multi-GPU partition) rendered separately equal the full frame."""
+@pytest.mark.parametrize("G,spp", [(3, 2), (8, 8)])
+def test_row_slices_compose(gpu, G, spp):
+    """Row-cyclic slices (multi-GPU partition) rendered separately equal the full frame
+    (G = 8 also switches the slices to one-row pixel groups)."""
     s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 96)
-    full = s.render(spp=2, want=("rgba", "hit_inst"))
-    G = 3
+    full = s.render(spp=spp, want=("rgba", "hit_inst"))
     out = np.zeros_like(full["rgba"])
     for r in range(G):
-        part = s.render(spp=2, row0=r, row_step=G, compact=True, want=("rgba",))
+        part = s.render(spp=spp, row0=r, row_step=G, compact=True, want=("rgba",))
         out[r::G] = part["rgba"]
     assert np.array_equal(out, full["rgba"])
 
