@@ -171,7 +171,8 @@ struct BvhRefs {
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
 #ifndef RT_TPC
-#define RT_TPC 2             // work indices claimed per ticket (trace_kernel's group loop)
+#define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop);
+                             // 3 vs 2: -0.8% world8_stress, -1.3% world8 (profiles/r01/ab_tpc_v33.log)
 #endif
 constexpr int TPC = RT_TPC;
 #ifndef RT_SHADE_LDS
