@@ -250,7 +250,10 @@ def main():
                                                           " textured" if args.textures else ""),
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bvh": use_bvh,
                    "parallelism": ("row-cyclic x%d + %s gather" % (world, "gloo host-staged" if gloo else "RCCL"))
-                                  if world > 1 else "single GPU"},
+                                  if world > 1 else "single GPU",
+                   # HIP hardware queues per process (HIP's and the pool's default is 4; bench.py sets 8
+                   # so that four render streams + main + collective each get a queue)
+                   "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1},
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
         "cold_frame_ms": round(cold_ms, 4), "frame_latency_ms": round(lat_ms, 4), "frames_in_flight": depth if overlap else 1,
         "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),

@@ -1665,6 +1665,13 @@ struct rt_scene {
     // through n copies of the per-frame state (BVH, work counters, scheduling history), so a
     // frame on another stream can start on CUs freed by the previous frames' tails.  The
     // fields above always hold the current slot; store[i] the others (store[cur] is stale).
+    // Instance arrays are per-slot state too (rt_builder_set_trans after finish): a frame in
+    // flight keeps the poses its BVH was built from, and the next frame of a slot receives the
+    // current poses by a stream-ordered copy (sync_slot_insts) from the slot's pinned staging.
+    DInst* h_insts_pin = nullptr; float4* h_inst4_pin = nullptr;   // current slot's staging (pinned)
+    unsigned slot_inst_gen = 0;                  // instance generation the current slot's arrays hold
+    unsigned inst_gen = 1;                       // generation of the host instance array (set_trans bumps it)
+    unsigned shape_gen = 0;                      // generation n_real / fdepth were computed for
     static constexpr int MAX_SLOTS = 4;
     struct Slot {
         Box* d_tree = nullptr; float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_fnode = nullptr;
@@ -1673,9 +1680,14 @@ struct rt_scene {
         unsigned long long* d_hctl = nullptr;
         int hist_cap = 0, hist_parity = 0, hctl_zeroed = -1;
         long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+        DInst* d_insts = nullptr; float4* d_inst4 = nullptr;
+        DInst* h_insts_pin = nullptr; float4* h_inst4_pin = nullptr;
+        unsigned slot_inst_gen = 0;
     } store[MAX_SLOTS];
     int n_slots = 1, cur_slot = 0;
-    hipEvent_t slot_done[MAX_SLOTS] = {};            // last frame of each slot (recorded on its stream)
+    // Last frame of each slot (recorded on its stream, also with one slot): the next frame of
+    // the slot, and side entries (debug_cast, experiments), wait for it stream-ordered.
+    hipEvent_t slot_done[MAX_SLOTS] = {};
     bool slot_pending[MAX_SLOTS] = {};
     ~rt_scene();
 };
@@ -1692,6 +1704,9 @@ void select_slot(rt_scene* s, int i) {
         f(s->d_hctl, o.d_hctl); f(s->hist_cap, o.hist_cap); f(s->hist_parity, o.hist_parity);
         f(s->hctl_zeroed, o.hctl_zeroed);
         for (int k = 0; k < 8; k++) f(s->hist_key[k], o.hist_key[k]);
+        f(s->d_insts, o.d_insts); f(s->d_inst4, o.d_inst4);
+        f(s->h_insts_pin, o.h_insts_pin); f(s->h_inst4_pin, o.h_inst4_pin);
+        f(s->slot_inst_gen, o.slot_inst_gen);
     };
     move(s->store[s->cur_slot], true);
     move(s->store[i], false);
@@ -1873,6 +1888,7 @@ int upload(rt_scene* s) {
     size_t nl = std::max(1, s->n_leaf);
     HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
     ordered_tree_shape(h, &s->n_real, &s->fdepth);
+    s->shape_gen = s->inst_gen;
     HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
@@ -1884,22 +1900,75 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_stats, 24 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
+    for (auto& e : s->slot_done) if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    s->slot_inst_gen = s->inst_gen;
     s->uploaded = true;
     if (s->n_slots > 1) return ensure_other_slot(s);
     return RT_OK;
 }
 
 // compact instance records for the trace kernel: (p, mesh | 0x80000000 when the pose is not identity)
-int upload_inst4(rt_scene* s) {
-    const rt::Scene& h = s->h;
-    std::vector<float4> v(h.d_insts.size());
-    for (size_t i = 0; i < v.size(); i++) {
+void fill_inst4(const rt::Scene& h, float4* v) {
+    for (size_t i = 0; i < h.d_insts.size(); i++) {
         const DInst& d = h.d_insts[i];
         uint32_t w = (uint32_t)d.mesh | (d.pose.identity ? 0u : 0x80000000u);
         float fw; memcpy(&fw, &w, 4);
         v[i] = make_float4(d.pose.p.x, d.pose.p.y, d.pose.p.z, fw);
     }
+}
+int upload_inst4(rt_scene* s) {
+    std::vector<float4> v(s->h.d_insts.size());
+    fill_inst4(s->h, v.data());
     if (!v.empty()) HIPCHK(hipMemcpy(s->d_inst4, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+// Bring the current slot's instance arrays to the host's generation, stream-ordered on `st`
+// (after the slot's previous frame, which the caller has made `st` wait for).  The pinned
+// staging is rewritten only once the copy that last read it has run (the slot's last frame,
+// recorded after that copy).
+int sync_slot_insts(rt_scene* s, hipStream_t st) {
+    if (s->slot_inst_gen == s->inst_gen) return RT_OK;
+    const size_t n = s->h.d_insts.size();
+    if (n) {
+        if (!s->h_insts_pin) {
+            HIPCHK(hipHostMalloc((void**)&s->h_insts_pin, n * sizeof(DInst), hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void**)&s->h_inst4_pin, n * sizeof(float4), hipHostMallocDefault));
+        } else if (s->slot_pending[s->cur_slot]) {
+            HIPCHK(hipEventSynchronize(s->slot_done[s->cur_slot]));
+        }
+        memcpy(s->h_insts_pin, s->h.d_insts.data(), n * sizeof(DInst));
+        fill_inst4(s->h, s->h_inst4_pin);
+        HIPCHK(hipMemcpyAsync(s->d_insts, s->h_insts_pin, n * sizeof(DInst), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(s->d_inst4, s->h_inst4_pin, n * sizeof(float4), hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(s->slot_done[s->cur_slot], st));   // covers the staging until the frame records it again
+        s->slot_pending[s->cur_slot] = true;
+    }
+    s->slot_inst_gen = s->inst_gen;
+    return RT_OK;
+}
+
+// Ordered-LBVH shape (leaf count, depth) for the current host poses: instances that moved
+// change the Morton order and with it the tree depth the fast traversal's stack must hold.
+void refresh_shape(rt_scene* s) {
+    if (s->shape_gen == s->inst_gen) return;
+    int nr = 0;
+    ordered_tree_shape(s->h, &nr, &s->fdepth);
+    s->shape_gen = s->inst_gen;
+}
+
+// Begin a frame on the current slot: `st` waits for the slot's previous frame (all slots'
+// last frames for side entries that do not rotate slots), then the slot's instances are
+// brought up to date.  end_frame records the slot's completion.
+int begin_frame(rt_scene* s, hipStream_t st, bool all_slots) {
+    for (int i = 0; i < rt_scene::MAX_SLOTS; i++)
+        if (s->slot_pending[i] && (all_slots || i == s->cur_slot)) HIPCHK(hipStreamWaitEvent(st, s->slot_done[i], 0));
+    refresh_shape(s);
+    return sync_slot_insts(s, st);
+}
+int end_frame(rt_scene* s, hipStream_t st) {
+    HIPCHK(hipEventRecord(s->slot_done[s->cur_slot], st));
+    s->slot_pending[s->cur_slot] = true;
     return RT_OK;
 }
 
@@ -1914,9 +1983,11 @@ int ensure_other_slot(rt_scene* s) {
         HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
         HIPCHK(hipMalloc((void**)&o.d_work, 16 * (NQ + 1) * sizeof(int)));
+        HIPCHK(hipMalloc((void**)&o.d_insts, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(DInst)));
+        HIPCHK(hipMalloc((void**)&o.d_inst4, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(float4)));
+        o.slot_inst_gen = 0;                                 // filled by sync_slot_insts on first use
         o.work_zeroed = false; o.bvh_valid = false;
     }
-    for (int i = 0; i < s->n_slots; i++) if (!s->slot_done[i]) HIPCHK(hipEventCreateWithFlags(&s->slot_done[i], hipEventDisableTiming));
     return RT_OK;
 }
 
@@ -2214,12 +2285,16 @@ rt_scene::~rt_scene() {
     for (auto& p : d_out) dfree(p);
     for (auto& e : ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : tev) (void)hipEventDestroy(e);
+    auto hfree = [](auto*& p) { if (p) { (void)hipHostFree(p); p = nullptr; } };
+    hfree(h_insts_pin); hfree(h_inst4_pin);
     for (int i = 0; i < MAX_SLOTS; i++) {                      // store[cur_slot] is the (freed) current state
         if (i == cur_slot) continue;
         Slot& o = store[i];
         dfree(o.d_tree); dfree(o.d_node_pair); dfree(o.d_leaf); dfree(o.d_fnode); dfree(o.d_work);
         for (int p = 0; p < 2; p++) { dfree(o.d_hlist[p]); dfree(o.d_hflag[p]); }
         dfree(o.d_hctl);
+        dfree(o.d_insts); dfree(o.d_inst4);
+        hfree(o.h_insts_pin); hfree(o.h_inst4_pin);
     }
     for (auto& e : slot_done) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -2320,13 +2395,11 @@ int rt_builder_set_trans(rt_scene* s, int t, const float* pos, const float* q) {
     if (t < 0 || t >= (int)s->h.insts.size()) return fail(RT_ERR_ARG, "transformation index out of range");
     if (pos) s->h.insts[t].pos = v3(pos[0], pos[1], pos[2]);
     if (q) s->h.insts[t].rot = Q{q[0], q[1], q[2], q[3]};
-    if (s->finished) {   // instances moved after finishing: refresh the flat copy and the device copy
+    if (s->finished) {   // instances moved after finishing: refresh the flat copy
+        // Device copies are per frame slot and are refreshed, stream-ordered, by the next frame
+        // of each slot (sync_slot_insts): frames in flight keep the poses they were built from.
         s->h.d_insts[t].pose = make_pose(s->h.insts[t].rot, s->h.insts[t].pos);
-        if (s->uploaded) {
-            HIPCHK(hipMemcpy(s->d_insts + t, &s->h.d_insts[t], sizeof(DInst), hipMemcpyHostToDevice));
-            int r = upload_inst4(s);
-            if (r != RT_OK) return r;
-        }
+        s->inst_gen++;
         invalidate(s);
     }
     return RT_OK;
@@ -2540,8 +2613,8 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     if (s->n_slots > 1) {                                    // rotate frame slots (rt_scene_set_frame_slots)
         if ((r = ensure_other_slot(s)) != RT_OK) return r;
         select_slot(s, (s->cur_slot + 1) % s->n_slots);
-        if (s->slot_pending[s->cur_slot]) HIPCHK(hipStreamWaitEvent(st, s->slot_done[s->cur_slot], 0));
     }
+    if ((r = begin_frame(s, st, false)) != RT_OK) return r;  // after the slot's previous frame, current poses
     if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st, te ? te[0] : nullptr, te ? te[1] : nullptr)) != RT_OK) {
@@ -2574,10 +2647,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         return r;
     }
     if (timed) HIPCHK(hipEventRecord(s->ev[2], st));
-    if (s->n_slots > 1) {                                    // the slot is free again once this frame is done
-        HIPCHK(hipEventRecord(s->slot_done[s->cur_slot], st));
-        s->slot_pending[s->cur_slot] = true;
-    }
+    if ((r = end_frame(s, st)) != RT_OK) return r;           // the slot is free again once this frame is done
     if (o->sync || timed || o->host_outputs) HIPCHK(hipStreamSynchronize(st));
     if (o->host_outputs) {
         if (o->rgba) HIPCHK(hipMemcpy(o->rgba, oo.rgba, out_px * 4, hipMemcpyDeviceToHost));
@@ -2667,12 +2737,15 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, 1)) != RT_OK) return r;
+    // rebuilds the current slot's BVH: first wait for every frame in flight (any slot)
+    if ((r = begin_frame(s, sstream(s), true)) != RT_OK) return r;
     if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
     HIPCHK(hipMemsetAsync(s->d_dbg, 0, 4096 * sizeof(int), sstream(s)));
     rt_render_opts o;
     rt_render_opts_default(&o);
     o.row0 = y; o.row_step = s->h.cam.H;                                  // just the row of (x, y)
     if ((r = launch_trace(s, o, sstream(s), s->d_canvas, s->d_dbg, x, y, true)) != RT_OK) return r;
+    if ((r = end_frame(s, sstream(s))) != RT_OK) return r;
     std::vector<int> log(4096);
     HIPCHK(hipStreamSynchronize(sstream(s)));
     HIPCHK(hipMemcpy(log.data(), s->d_dbg, log.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -2698,6 +2771,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         HIPCHK(hipSetDevice(s->device));
         if ((r = ensure_spp(s, spp)) != RT_OK) return r;
         rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
+        if ((r = begin_frame(s, sstream(s), true)) != RT_OK) return r;   // nothing else in flight on this slot
         if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
@@ -2713,6 +2787,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
             float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
             if (i > 0 || reps == 1) total += t;
         }
+        if ((r = end_frame(s, sstream(s))) != RT_OK) return r;
         unsigned long long v[22];
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
         if (counters) for (int i = 0; i < 22; i++) counters[i] = v[i];
@@ -2722,6 +2797,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((r = ensure_spp(s, spp)) != RT_OK) return r;
+    if ((r = begin_frame(s, sstream(s), true)) != RT_OK) return r;
     if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
     s->work_zeroed = false;                                  // the primary kernels reset d_work themselves
     rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
@@ -2757,6 +2833,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
         if (i > 0 || reps == 1) total += t;
     }
+    if ((r = end_frame(s, sstream(s))) != RT_OK) return r;
     unsigned long long v[22];
     HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
     if (counters) for (int i = 0; i < 22; i++) counters[i] = v[i];
@@ -2791,6 +2868,7 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, in
     geo[0] = geo[1] = geo[2] = geo[3] = 0;
     reps = std::max(reps, 2);                                 // frame 0 sizes the buffer and seeds the history
     const int nw = prof ? 10 : 1;                             // prof: + 9 counters per group (PROF kernel)
+    if ((r = begin_frame(s, sstream(s), true)) != RT_OK) { (void)hipFree(d_rgba); return r; }
     for (int i = 0; i < reps && r == RT_OK; i++) {
         const bool rec = i == reps - 1;
         if (rec) {
@@ -2802,6 +2880,7 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, in
         r = launch_trace(s, o, sstream(s), d_rgba, nullptr, -1, -1, false, -1, s->ev[0], s->ev[1], rec && prof,
                          rec ? d_g : nullptr, geo);
     }
+    if (r == RT_OK) r = end_frame(s, sstream(s));
     if (r == RT_OK) {
         HIPCHK(hipEventSynchronize(s->ev[1]));
         float t = 0;

@@ -79,3 +79,56 @@ def test_pipeline_world2_gather_and_unpermute(gpu):
                                                      rgba_ptr=buf.data_ptr(), stream=st.cuda_stream))
     torch.cuda.synchronize()
     assert torch.equal(pipe.finish(), full)
+
+
+def _move(s, k, inst):
+    """Frame k's poses: a few instances lifted / shifted (cumulative), one frame with a
+    rotated instance (the general-pose kernels), so consecutive frames differ."""
+    n = inst.shape[0]
+    for j in range(3):
+        t = (37 * k + 101 * j) % n
+        p = inst[t, 4:7] + np.float32([0.25 * j, 0.5 + 0.125 * k, -0.25 * j])
+        s.set_trans(t, pos=p)
+    if k == 5:
+        s.set_trans(11, quat=(0.0, 0.38268343, 0.0, 0.9238795))      # 45 deg about y
+    if k == 7:
+        s.set_trans(11, quat=(0.0, 0.0, 0.0, 1.0))
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_pipeline_moving_instances(gpu, depth):
+    """rt_builder_set_trans between frames in flight: every frame of the
+    pipeline equals the serial render of the same poses; a debug_cast side entry in the
+    middle (it rebuilds the current slot's BVH) disturbs no frame."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+    import rtamd.dist as rtdist
+    w, h, spp, n_frames = 160, 120, 2, 9
+    ser = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    inst = ser.export("instances").copy()
+    refs = []
+    for k in range(n_frames):
+        _move(ser, k, inst)
+        buf = torch.zeros((h, w), dtype=torch.int32, device="cuda")
+        ser.render_device(spp=spp, rgba_ptr=buf.data_ptr(), sync=True)
+        refs.append(buf)
+    assert not all(torch.equal(refs[0], r) for r in refs[1:])   # the poses change the frames
+    s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    s.set_frame_slots(depth)
+    pipe = rtdist.FramePipeline(w, h, 1, 0, "cuda", depth=depth)
+    outs = [None] * n_frames
+
+    def render(k):
+        def f(buf, st):
+            s.render_device(spp=spp, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream)
+            outs[k] = buf.clone()                                  # on st, after the render
+        return f
+    for k in range(n_frames):
+        _move(s, k, inst)
+        pipe.step(k, render(k))
+        if k == 4:
+            s.debug_cast(w // 2, h // 2)
+    pipe.finish()
+    torch.cuda.synchronize()
+    for k in range(n_frames):
+        assert torch.equal(outs[k], refs[k]), k
