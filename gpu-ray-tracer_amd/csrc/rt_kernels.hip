@@ -85,6 +85,27 @@ __device__ __forceinline__ float pow_fast(float x, float y) {
 
 
 
+// Unsigned division by a launch constant d with host-computed magic numbers (round-up
+// method: l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, q = (t + ((n - t) >> 1)) >> (l - 1),
+// t = mulhi(n, m); exact for every 32-bit n; d = 1 passes through).  Wave-uniform operands stay
+// on the scalar unit (the compiler's own sequence keeps a VGPR reciprocal live across the
+// group loop, which was spilled and reloaded from scratch at every group).
+struct UDiv { unsigned m, d; int s; };
+__host__ inline UDiv udiv_make(unsigned d) {
+    UDiv r{0u, d, 0};
+    if (d <= 1) return r;
+    int l = 0;
+    while ((1ull << l) < d) l++;
+    r.m = (unsigned)((((1ull << l) - d) << 32) / d + 1);
+    r.s = l - 1;
+    return r;
+}
+__device__ __forceinline__ unsigned udiv(unsigned n, const UDiv& D) {
+    if (D.d <= 1) return n;
+    const unsigned t = __umulhi(n, D.m);
+    return (t + ((n - t) >> 1)) >> D.s;
+}
+
 struct SceneView {           // read-only scene data (HBM, L2-resident)
     const DTri* __restrict__ tris;
     const DMesh* __restrict__ meshes;
@@ -167,6 +188,12 @@ struct BvhRefs {
     const DMesh* meshes;
 };
 
+#ifndef RT_EXP_NORED
+#define RT_EXP_NORED 0       // experiment builds only (group-overhead dissection), see tools/ab.sh
+#endif
+#ifndef RT_EXP_NOHIST
+#define RT_EXP_NOHIST 0
+#endif
 #ifndef RT_FILTERED
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
@@ -512,9 +539,10 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // (tree depth <= 31 is checked on the host): an internal node as its index, a
         // leaf B as -2 - parent, whose pair test is re-run when it is popped (fresh hit
         // and entry bound under the current cut).  Pruning and triangle skip as above.
+        // The per-query direction chain (dir_pre) is formed at the wave's first leaf visit:
+        // most queries (sky rays) reach no leaf, and it depends on the ray only.
         DirPre pre{};
-        if (AXIS) pre = dir_pre<true>(r.d);                      // S.tri_ax set: identity rotations
-        else if (S.ident_all) pre = dir_pre(r.d);
+        bool pre_ok = false;                                   // wave-uniform
         const bool box_bound = S.prune_abs >= 0.0f;
         auto t_low = [&](float tl) { return box_bound ? tl - slack(tl) : -INFINITY; };
         // One pair-test site and one leaf site (the leaf code is the bulk of the kernel):
@@ -538,9 +566,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 bool h0, h1;
                 float t0, t1;
                 if (PROF) wc.wpair++;
-                pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
-                const float4 rf = rec[3];
+                // child references first, in the same LDS batch as the boxes: one round trip
+                // per step (read after the pair test, they cost a second dependent one)
+                const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
                 const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
+                pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
                 if (prune) {
                     const float ct = cut();
                     h0 = h0 && !(t0 > ct);
@@ -571,6 +601,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 }
             }
             if (linst >= 0 && __ballot(lh)) {
+                if (!pre_ok) {
+                    if (AXIS) pre = dir_pre<true>(r.d);        // S.tri_ax set: identity rotations
+                    else if (S.ident_all) pre = dir_pre(r.d);
+                    pre_ok = true;
+                }
                 const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
                 if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
                 if (lh && cast_local<false, AXIS, PROF>(S, bv, uni(linst), r, b, pre, wc, t_low(ltl))) {
@@ -689,7 +724,10 @@ struct TraceParams {
     V3 dist_atten;
     V4 ambience;
     int W, H, row0, row_step, n_rows, compact, spp, depth;
+    float spp_recip;          // 2^-k when spp = 2^k (exact reciprocal), else 0
     int lanes_per_px, px_per_wave, gw, gh, n_gx, n_groups;   // sample-parallel lane mapping
+    int l_shift, gw_shift;    // log2(lanes_per_px), log2(gw) when powers of two, else -1
+    UDiv div_ngx, div_perq;   // g / n_gx and ticket permutation mod per-queue length
     int scramble;             // ticket -> group permutation factor (coprime with the queue length)
     int scramble_small;       // 1: ticket * scramble < 2^32 for every ticket (32-bit modulo)
     const float2* __restrict__ spp_off;
@@ -715,13 +753,37 @@ struct TraceParams {
     unsigned* gdur;           // profiling (rt_profile_groups): per-group duration, 100 MHz ticks; NULL normally
 };
 
+// The launch's TraceParams read in place from the kernel-argument segment (constant address
+// space: scalar loads) through a pointer made fresh at each use site.  Passed by value and
+// used directly, its ~80 dwords were loaded once and held in SGPRs for the whole persistent
+// kernel; the scalar register file overflowed into VGPR lanes, and every group and every
+// state-machine step re-read them with v_readlane (VALU issue slots).  Fresh per scope, a
+// field is loaded (s_load) where it is needed and its SGPRs are free elsewhere.
+typedef __attribute__((address_space(4))) const TraceParams KTP;
+// a struct field of the in-place parameters, copied to registers word by word (scalar loads)
+template <class T> __device__ __forceinline__ T kld(const __attribute__((address_space(4))) T& x) {
+    static_assert(sizeof(T) % 4 == 0, "4-byte granular");
+    T r;
+    const __attribute__((address_space(4))) uint32_t* src = (const __attribute__((address_space(4))) uint32_t*)&x;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(T) / 4); w++) d[w] = src[w];
+    return r;
+}
+__device__ __forceinline__ KTP& kparams() {
+    KTP* p = (KTP*)__builtin_amdgcn_kernarg_segment_ptr();     // the first kernel argument
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
 // Textured mode (build-defined; phong.cu:18-23 leaves texture mapping a TODO): the
 // diffuse colour of a hit on a triangle with TextureCoords is the atlas texel at
 // (tx, ty) + u (ux, uy) + v (vx, vy), clamped to the atlas and truncated to a texel
 // index (point sampling, clamp addressing: the reference's texture setup); other hits
 // keep the material's Kd.  gfx950 has no image/sampler instructions (HIP marks tex2D
 // unavailable there), so the atlas is a plain float4 array in HBM.
-__device__ __forceinline__ V4 hit_kd(const TraceParams& P, const BvhRefs& bv, const Best& b, int mat) {
+template <class PT>
+__device__ __forceinline__ V4 hit_kd(const PT& P, const BvhRefs& bv, const Best& b, int mat) {
     const DTri& T = bv.tris[b.tri];
     if (!T.tex) return bv.mats[mat].Kd;
     const float x = (T.tx + b.u * T.ux) + b.v * T.vx;
@@ -735,8 +797,21 @@ __device__ __forceinline__ V4 hit_kd(const TraceParams& P, const BvhRefs& bv, co
 // Opaque to the optimiser: values derived from x (64-bit output addresses) are formed
 // here instead of being hoisted to the group start and spilled across the trace.
 __device__ __forceinline__ void opaque(int& x) { asm volatile("" : "+v"(x)); }
+// A wave-uniform value made loop-variant where it is used: per-group constants derived from
+// it (camera terms of the kernel arguments) are recomputed there instead of being hoisted out
+// of the persistent group loop, held in VGPRs across the trace and spilled (the spill reloads
+// were long-latency scratch misses at every group start).
+template <class T> __device__ __forceinline__ T fresh_s(T x) { asm volatile("" : "+s"(x)); return x; }
 
-__device__ __forceinline__ void dbg(const TraceParams& P, bool me, int ev) {
+// Build-defined sample offset k (rt_scene.cpp spp_offset: R2 sequence in double), computed
+// with the same correctly rounded double operations as the host table.
+__device__ __forceinline__ float2 spp_offset_dev(int k) {
+    const double u = (double)k * 0.7548776662466927, v = (double)k * 0.5698402909980532;
+    return make_float2((float)(u - floor(u)), (float)(v - floor(v)));
+}
+
+template <class PT>
+__device__ __forceinline__ void dbg(const PT& P, bool me, int ev) {
     if (P.dbg_log && me) {
         int i = atomicAdd(P.dbg_log, 1);
         if (i < 4094) P.dbg_log[2 + i] = ev;
@@ -770,8 +845,9 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // stop the compiler from forwarding the stored values and keeping them live.
 constexpr int PARK_FIELDS = 25;
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
-__device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView& S, const BvhRefs& bv, bool valid,
+__device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
+    KTP& P0 = kparams();
     Frame cur;
     SavedFrame stk[NS > 0 ? NS : 1];
     int top = -1, st = ST_DONE;
@@ -791,7 +867,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     if (valid) {
         cur.ray = r0;
         cur.atten = v4(1.0f, 1.0f, 1.0f, 1.0f); cur.last_mat = -1;
-        cur.type = F_NORMAL; cur.depth = P.depth; cur.in_obj = 0;
+        cur.type = F_NORMAL; cur.depth = P0.depth; cur.in_obj = 0;
         top = 0; st = ST_ADVANCE;
     }
     auto pop = [&]() {
@@ -800,6 +876,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
     };
     unsigned long long c_post = 0;
     for (;;) {
+        KTP& P = kparams();
         if ((STATS || PROF) && c_post) { wc.cyc_post += __builtin_amdgcn_s_memtime() - c_post; c_post = 0; }
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
@@ -944,7 +1021,7 @@ __device__ __forceinline__ V4 trace_sample(const TraceParams& P, const SceneView
                 fl |= 2;                                           // popped after illumination (frame still needed)
             }
             const DMat& m = bv.mats[is_mat];                       // org_light (phong.cu:36-39)
-            summed = m.Ke + m.Ka * P.ambience;
+            summed = m.Ke + m.Ka * kld(P.ambience);
             li = 0;
             st = ST_LIGHT;
             continue;
@@ -1058,14 +1135,15 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
 constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128;
 template <int NS, bool LDS, int MODE>
-__global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, SceneView S) {
+__global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    (void)P_arg;                                               // read in place: kparams()
+    KTP& P = kparams();
     constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
     constexpr bool SHADE = (MODE & M_SHADE) != 0;
     const BvhRefs bv = stage_bvh<LDS, FT, SHADE>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
-    const int pix = lane / L, sub = lane - pix * L, base = lane - sub;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
@@ -1096,7 +1174,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     int pend = 0, inflight = 0;
     auto step_of = [&](int q) { return q < 0 ? 1 : TPC; };
     auto request = [&](int q) {
-        if (lane == 0) pend = atomicAdd(q < 0 ? &P.work[16 * NQ] : &P.work[16 * ((q0 + q) % NQ)], step_of(q));
+        KTP& Pq = kparams();
+        if (lane == 0) pend = atomicAdd(q < 0 ? &Pq.work[16 * NQ] : &Pq.work[16 * ((q0 + q) % NQ)], step_of(q));
         inflight = 1;
     };
     auto resolve = [&]() { inflight = 0; return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
@@ -1105,6 +1184,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
     const unsigned long long c_start = CYC ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long rt_start = CYC ? __builtin_amdgcn_s_memrealtime() : 0;   // global 100 MHz clock
     for (;;) {
+        KTP& P = kparams();                                    // this group's reads of the launch parameters
         for (;;) {                                             // next work index tbase + j of queue qi
             if (qi >= NQ) break;
             const int lim = qi < 0 ? n_heavy : per_q;
@@ -1125,36 +1205,58 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
         // bijection): expensive image regions are spread over the frame instead of all
         // starting last and leaving a long tail of idle CUs (measured: first wave done at
         // 69% of the kernel span with row order)
-        const int g = qi < 0 ? uni(P.hl_prev[ticket])
-                             : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)(((unsigned)ticket * (unsigned)P.scramble) % (unsigned)per_q)
+        // The scheduling history is read with scalar loads: a vector load here would wait
+        // (vmcnt is in order) for the previous group's output stores to be acknowledged.
+        auto umod = [&](unsigned n) { return n - udiv(n, kld(P.div_perq)) * (unsigned)per_q; };
+        const int g = qi < 0 ? ldc(P.hl_prev, ticket)
+                             : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)umod((unsigned)ticket * (unsigned)P.scramble)
                                                                          : (int)(((long long)ticket * P.scramble) % per_q));
-        if (g >= P.n_groups || (qi >= 0 && P.hist && P.hf_prev[g])) continue;
+        if (g >= P.n_groups || (qi >= 0 && P.hist && ((ldc(reinterpret_cast<const uint32_t*>(P.hf_prev), g >> 2) >> (8 * (g & 3))) & 0xffu)))
+            continue;
         const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
-        const int gx = g % P.n_gx, gy = g / P.n_gx;
-        const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
-        const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows;
+        const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
+        // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
+        // kept live across the trace
+        int ln = lane;
+        opaque(ln);
+        const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
+        const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
+        const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
+        const int sub_g = P.l_shift >= 0 ? ln & (L - 1) : ln - pix_g * L, base_g = ln - sub_g;
+        const int px = gx * P.gw + pxo, pr = gy * P.gh + pyo;
+        const bool valid = pix_g < P.px_per_wave && px < P.W && pr < P.n_rows;
         const int py = P.row0 + pr * P.row_step;
         const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
-        const bool me = valid && sub == 0 && px == P.dbg_x && py == P.dbg_y;
+        const bool me = valid && sub_g == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
         const unsigned long long g_c0 = wc.cyc_q, g_c1 = wc.cyc_leaf, g_c2 = wc.cyc_sample, g_c3 = wc.cyc_post;
         const unsigned long long g_m0 = CYC ? __builtin_amdgcn_s_memtime() : 0;
         for (int rd = 0; rd < rounds; rd++) {
-            const int k = rd * L + sub;
+            const int k = rd * L + sub_g;
             const bool act = valid && k < P.spp;
             Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
             if (act) {
-                float2 o = P.spp_off[k];
-                r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
+#if RT_EXP_TAB
+                const float2 o = P.spp_off[k];
+#else
+                const float2 o = spp_offset_dev(k);
+#endif
+#if RT_EXP_NOCAM                                               // experiment: no camera ray
+                r0.d = v3((float)px + o.x, (float)py + o.y, 1.0f);
+#else
+                DCamera cam = kld(P.cam);
+                cam.W = fresh_s(cam.W); cam.H = fresh_s(cam.H); cam.near_ = fresh_s(cam.near_);
+                r0 = camera_at(cam, (float)px + o.x, (float)py + o.y);
+#endif
             }
             if (rd == 0 && last_of_batch) request(qi);         // next ticket, in flight during the trace
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
 #if RT_EXP_NOTRACE                                             // experiment: group overhead only
             V4 c = v4(r0.d.x, r0.d.y, r0.d.z, 1.0f);
 #else
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(P, S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
 #endif
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
@@ -1163,30 +1265,49 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P, Sce
             };
             // in-order reduction over samples (ds_bpermute: the LDS pipe has room, the VALU
             // does not -- a DPP row-shift form measured 4% slower)
-            for (int s = 0; s < L; s++) {
-                V4 v = shfl4(c, base + s);
-                if (sub == 0 && rd * L + s < P.spp) {
-                    sum_c = sum_c + clamp1(v);
-                    sum_r = sum_r + v;
+            if (RT_EXP_NORED) {                                // experiment: no sample reduction
+                sum_c = sum_c + c;
+            } else if (L == 8) {                               // spp = 8: all 32 permutes in one LDS round trip
+                V4 v[8];
+#pragma unroll
+                for (int s = 0; s < 8; s++) v[s] = shfl4(c, base_g + s);
+#pragma unroll
+                for (int s = 0; s < 8; s++)
+                    if (sub_g == 0 && rd * L + s < P.spp) {
+                        sum_c = sum_c + clamp1(v[s]);
+                        sum_r = sum_r + v[s];
+                    }
+            } else {
+                for (int s = 0; s < L; s++) {
+                    V4 v = shfl4(c, base_g + s);
+                    if (sub_g == 0 && rd * L + s < P.spp) {
+                        sum_c = sum_c + clamp1(v);
+                        sum_r = sum_r + v;
+                    }
                 }
             }
         }
-        if (valid && sub == 0) {
+        if (valid && sub_g == 0) {
+            KTP& P = kparams();
             int p = pix_index;
             opaque(p);                                         // address math stays here, not live across the trace
             const float inv = (float)P.spp;
-            const float mr = sum_c.x / inv, mg = sum_c.y / inv, mb = sum_c.z / inv, ma = sum_c.w / inv;
+            // mean = sum / spp (raytracer.cu's per-sample colour, build-defined spp average);
+            // for spp = 2^k, x * 2^-k is the same correctly rounded value as x / 2^k
+            auto mean = [&](float x) { return P.spp_recip != 0.0f ? x * P.spp_recip : x / inv; };
+            const float mr = mean(sum_c.x), mg = mean(sum_c.y), mb = mean(sum_c.z), ma = mean(sum_c.w);
             // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
             const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
                                  ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
             if (P.rgba) P.rgba[p] = enc;
-            if (P.radiance) P.radiance[p] = make_float4(sum_r.x / inv, sum_r.y / inv, sum_r.z / inv, sum_r.w / inv);
+            if (P.radiance) P.radiance[p] = make_float4(mean(sum_r.x), mean(sum_r.y), mean(sum_r.z), mean(sum_r.w));
         }
         if (STATS && P.stats && lane == 0) {                 // profiling: heaviest group (PROF: rt_profile_groups)
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
-        if (P.hist && lane == 0) {                            // record for the next frame's order
+        if (kparams().hist && lane == 0) {                     // record for the next frame's order
+            KTP& P = kparams();
             const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;
             const bool heavy = dur > thr;
             P.hf_next[g] = heavy ? 1 : 0;
@@ -2141,6 +2262,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         return RT_OK;
     }
     P.compact = o.compact; P.spp = o.spp; P.depth = h.depth;
+    P.spp_recip = (o.spp & (o.spp - 1)) == 0 ? 1.0f / (float)o.spp : 0.0f;
     P.spp_off = s->d_spp;
     P.rgba = rgba; P.radiance = reinterpret_cast<float4*>(o.radiance); P.hit_inst = o.hit_inst; P.hit_tri = o.hit_tri;
     P.stats = (want_stats || prof) ? s->d_stats : nullptr; P.dbg_log = dbg; P.dbg_x = dbg_x; P.dbg_y = dbg_y;
@@ -2165,17 +2287,21 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     if (P.px_per_wave % RT_GROUP_W == 0) gw = RT_GROUP_W;
 #endif
     P.gw = gw; P.gh = P.px_per_wave / gw;
+    auto log2_exact = [](int v) { int k = 0; while ((1 << k) < v) k++; return (1 << k) == v ? k : -1; };
+    P.l_shift = log2_exact(P.lanes_per_px); P.gw_shift = log2_exact(P.gw);
     P.n_gx = (P.W + P.gw - 1) / P.gw;
     P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
     if (geo) { geo[0] = P.n_groups; geo[1] = P.gw; geo[2] = P.gh; geo[3] = P.n_gx; }
     P.scramble = ticket_scramble((P.n_groups + NQ - 1) / NQ);
     P.scramble_small = (unsigned long long)((P.n_groups + NQ - 1) / NQ + TPC) * (unsigned long long)P.scramble < (1ull << 32);
+    P.div_ngx = udiv_make((unsigned)P.n_gx);
+    P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * (NQ + 1) * sizeof(int), st));
     // longest-first history (fast frames): valid while the launch layout is unchanged
     P.hist = 0;
-    if (!want_stats && !dbg) {
+    if (!want_stats && !dbg && !RT_EXP_NOHIST) {
         const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
         int r;
         if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
