@@ -445,6 +445,40 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
     return vec_from_local(ip, n);
 }
 
+// Zero direction components (box bound, see closest_hit).  The reference's slab test
+// skips an axis with d_a == 0 (bounding_box.cu:62-104), so such a ray "hits" every
+// box its other coordinates cross, whatever o_a: the shadow rays of the directional
+// light (0, -1, 1) and the primary rays of the centre column/row sweep whole rows
+// of leaves.  Along the ray the coordinate stays o_a exactly (world and local:
+// d_a and the local direction's component are 0), so an accepted hit lies within
+// the slack of the leaf box on that axis: a node whose a-range excludes o_a by more
+// than prune_abs has no acceptable hit below it (node boxes contain their leaves').
+// The slab then becomes [K (mn - o - M), K (mx - o + M)] through the same fma and
+// bias as a nonzero axis (pair_hit_at): both ends > 0 or < 0 exactly when o_a is
+// outside [mn - M, mx + M] (a certain miss), else lo_a <= 0 < 1e-5 <= hi_a never
+// binds (every nonzero axis bounds t by ~1e3; lo <= 0 is below any acceptable
+// time, so entry bounds stay valid).  closest_hit's `im` keeps the nonzero axes only.
+// Fast (ordered-LBVH) kernels only.
+__device__ __forceinline__ void zero_axis_cut(const SceneView& S, const Ray& r, RayInv& ri) {
+    if (!ZERO_AXIS_CUT || !(S.prune_abs >= 0.0f)) return;
+    constexpr float K = 0x1p32f;
+    if (r.d.x == 0.0f) { ri.ix = K; ri.bx = K * S.prune_abs; }
+    if (r.d.y == 0.0f) { ri.iy = K; ri.by = K * S.prune_abs; }
+    if (r.d.z == 0.0f) { ri.iz = K; ri.bz = K * S.prune_abs; }
+}
+
+// First step of the fast traversal for a ray (closest_hit, FT path, node 0 with an empty
+// closest hit): whether it hits either child of the ordered LBVH's root.  A lane for which
+// this is false visits nothing, and its query returns no hit.
+__device__ __forceinline__ bool ft_root_hit(const SceneView& S, const BvhRefs& bv, bool active, const Ray& r) {
+    RayInv ri = ray_inv(r);
+    zero_axis_cut(S, r, ri);
+    bool h0, h1;
+    float t0, t1;
+    pair_hit_at(bv.fnode, r, ri, active, h0, h1, t0, t1);
+    return h0 || h1;
+}
+
 // renv::gpu::cast_ray (scene.cu:42-73) for the whole wave.  Packet traversal of
 // the reference's implicit heap: at an internal node hit by some lane, both
 // children (2k, 2k+1: adjacent records) are tested; the wave descends into 2k
@@ -512,25 +546,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     const int n = S.n_leaf;
     RayInv ri = ray_inv(r);
     im = ri.exact ? INFINITY : fmaxf(fabsf(ri.ix), fmaxf(fabsf(ri.iy), fabsf(ri.iz)));
-    if (FT && ZERO_AXIS_CUT && S.prune_abs >= 0.0f) {
-        // Zero direction components (box bound, see above).  The reference's slab test
-        // skips an axis with d_a == 0 (bounding_box.cu:62-104), so such a ray "hits" every
-        // box its other coordinates cross, whatever o_a: the shadow rays of the directional
-        // light (0, -1, 1) and the primary rays of the centre column/row sweep whole rows
-        // of leaves.  Along the ray the coordinate stays o_a exactly (world and local:
-        // d_a and the local direction's component are 0), so an accepted hit lies within
-        // the slack of the leaf box on that axis: a node whose a-range excludes o_a by more
-        // than prune_abs has no acceptable hit below it (node boxes contain their leaves').
-        // The slab then becomes [K (mn - o - M), K (mx - o + M)] through the same fma and
-        // bias as a nonzero axis (pair_hit_at): both ends > 0 or < 0 exactly when o_a is
-        // outside [mn - M, mx + M] (a certain miss), else lo_a <= 0 < 1e-5 <= hi_a never
-        // binds (every nonzero axis bounds t by ~1e3; lo <= 0 is below any acceptable
-        // time, so entry bounds stay valid).  `im` keeps the nonzero axes only.
-        constexpr float K = 0x1p32f;
-        if (r.d.x == 0.0f) { ri.ix = K; ri.bx = K * S.prune_abs; }
-        if (r.d.y == 0.0f) { ri.iy = K; ri.by = K * S.prune_abs; }
-        if (r.d.z == 0.0f) { ri.iz = K; ri.bz = K * S.prune_abs; }
-    }
+    if (FT) zero_axis_cut(S, r, ri);
     if (FT) {
         // Ordered LBVH (fast kernel, S.ftree): same leaves and leaf order as the heap, so
         // each lane meets exactly the leaves its ray hits, in the heap's DFS order (a
@@ -700,6 +716,9 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
 // ---------------------------------------------------------------------------
 // kd: the material's Kd (the reference), or the atlas texel in the textured mode
 __device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
+#if RT_EXP_NOPHONG                                             // experiment: shading arithmetic priced (wrong colours)
+    return incoming + kd;
+#endif
     float nd = max_std(dot(to_light, nrm), 0.0f);
     V4 diffuse = nd * kd;
     V3 reflected = reflect(neg(to_light), nrm);
@@ -802,13 +821,13 @@ __device__ __forceinline__ void opaque(int& x) { asm volatile("" : "+v"(x)); }
 // of the persistent group loop, held in VGPRs across the trace and spilled (the spill reloads
 // were long-latency scratch misses at every group start).
 template <class T> __device__ __forceinline__ T fresh_s(T x) { asm volatile("" : "+s"(x)); return x; }
-
-// Build-defined sample offset k (rt_scene.cpp spp_offset: R2 sequence in double), computed
-// with the same correctly rounded double operations as the host table.
-__device__ __forceinline__ float2 spp_offset_dev(int k) {
-    const double u = (double)k * 0.7548776662466927, v = (double)k * 0.5698402909980532;
-    return make_float2((float)(u - floor(u)), (float)(v - floor(v)));
+// This lane's index, recomputed where it is used (two VALU) rather than held across the
+// persistent loop (it was spilled and reloaded from scratch at every group).
+__device__ __forceinline__ int lane_id_fresh() {
+    const unsigned m = fresh_s(~0u);
+    return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
 }
+
 
 template <class PT>
 __device__ __forceinline__ void dbg(const PT& P, bool me, int ev) {
@@ -1217,8 +1236,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
-        int ln = lane;
-        opaque(ln);
+        const int ln = lane_id_fresh();
         const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
         const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
         const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
@@ -1238,11 +1256,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             const bool act = valid && k < P.spp;
             Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
             if (act) {
-#if RT_EXP_TAB
                 const float2 o = P.spp_off[k];
-#else
-                const float2 o = spp_offset_dev(k);
-#endif
 #if RT_EXP_NOCAM                                               // experiment: no camera ray
                 r0.d = v3((float)px + o.x, (float)py + o.y, 1.0f);
 #else
@@ -1252,6 +1266,19 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
 #endif
             }
             if (rd == 0 && last_of_batch) request(qi);         // next ticket, in flight during the trace
+            // Whole-group miss (fast kernels): when no lane's primary ray hits a child of the
+            // tree's root -- the traversal's first step, same test -- every sample misses, its
+            // radiance is the integrator's initial zero (scene.cu:124-126) and the group's
+            // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
+            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && !__ballot(ft_root_hit(S, bv, act, r0))) {
+                if (act && k == 0) {
+                    int op = pix_index;
+                    opaque(op);
+                    if (P.hit_inst) P.hit_inst[op] = -1;
+                    if (P.hit_tri) P.hit_tri[op] = -1;
+                }
+                break;                                         // sum_c = sum_r = 0
+            }
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
 #if RT_EXP_NOTRACE                                             // experiment: group overhead only
             V4 c = v4(r0.d.x, r0.d.y, r0.d.z, 1.0f);
@@ -1264,27 +1291,45 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                 return v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y, v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);
             };
             // in-order reduction over samples (ds_bpermute: the LDS pipe has room, the VALU
-            // does not -- a DPP row-shift form measured 4% slower)
+            // does not -- a DPP row-shift form measured 4% slower).  Each lane clamps its own
+            // sample before the exchange (the same bits the leader would compute), and the raw
+            // sum is formed only when the radiance output is requested.
+            // (lane addresses and sample bounds formed here, after the trace: hoisted above it,
+            // they were held across the trace and spilled)
+            KTP& Pr = kparams();
+            const bool want_r = Pr.radiance != nullptr;
+            const int spp_n = Pr.spp;
+            int bb = base_g;
+            opaque(bb);
+            const V4 cc = clamp1(c);
             if (RT_EXP_NORED) {                                // experiment: no sample reduction
                 sum_c = sum_c + c;
-            } else if (L == 8) {                               // spp = 8: all 32 permutes in one LDS round trip
+            } else if (L == 8) {                               // spp = 8: all permutes in one LDS round trip
                 V4 v[8];
 #pragma unroll
-                for (int s = 0; s < 8; s++) v[s] = shfl4(c, base_g + s);
+                for (int s = 0; s < 8; s++) v[s] = shfl4(cc, bb + s);
+                if (sub_g == 0)
 #pragma unroll
-                for (int s = 0; s < 8; s++)
-                    if (sub_g == 0 && rd * L + s < P.spp) {
-                        sum_c = sum_c + clamp1(v[s]);
-                        sum_r = sum_r + v[s];
-                    }
+                    for (int s = 0; s < 8; s++)
+                        if (rd * L + s < spp_n) sum_c = sum_c + v[s];
+                if (want_r) {
+#pragma unroll
+                    for (int s = 0; s < 8; s++) v[s] = shfl4(c, bb + s);
+                    if (sub_g == 0)
+#pragma unroll
+                        for (int s = 0; s < 8; s++)
+                            if (rd * L + s < spp_n) sum_r = sum_r + v[s];
+                }
             } else {
                 for (int s = 0; s < L; s++) {
-                    V4 v = shfl4(c, base_g + s);
-                    if (sub_g == 0 && rd * L + s < P.spp) {
-                        sum_c = sum_c + clamp1(v);
-                        sum_r = sum_r + v;
-                    }
+                    const V4 v = shfl4(cc, bb + s);
+                    if (sub_g == 0 && rd * L + s < spp_n) sum_c = sum_c + v;
                 }
+                if (want_r)
+                    for (int s = 0; s < L; s++) {
+                        const V4 v = shfl4(c, bb + s);
+                        if (sub_g == 0 && rd * L + s < spp_n) sum_r = sum_r + v;
+                    }
             }
         }
         if (valid && sub_g == 0) {
@@ -1306,10 +1351,12 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
-        if (kparams().hist && lane == 0) {                     // record for the next frame's order
+        if (kparams().hist) {                                  // record for the next frame's order
             KTP& P = kparams();
-            const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;
+            const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;   // wave-uniform (scalar)
             const bool heavy = dur > thr;
+            wave_sum += dur;
+            if (lane_id_fresh() == 0) {
             P.hf_next[g] = heavy ? 1 : 0;
             if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
             if (P.gdur) {
@@ -1323,7 +1370,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                     c[8] = (unsigned)(__builtin_amdgcn_s_memtime() - g_m0);
                 }
             }
-            wave_sum += dur;
+            }
         }
     }
     if (P.hist && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
