@@ -221,10 +221,10 @@ __device__ __forceinline__ f2 vmax(f2 a, f2 b) { return f2{fmaxf(a.x, b.x), fmax
 
 // BoundingBox::intersects (bounding_box.cu:62-104) for both children of pair k.
 // Filtered like box_hit_f (rt_math.h), with the bound taken from the slab results
-// themselves: every quotient q' = fl(e * fl(1/d)) is within 3.01u |q| of the
-// reference's fl(e / d), min and max keep a relative bound (|max a' - max a| <=
-// 3.03u max(|a|, |a'|)), so |lo' - lo| <= 6.1u |lo'| and the same for hi; the test
-// uses 16u plus an absolute floor.  Zero direction components are skipped through
+// themselves: every quotient q' = fl(e * r'), r' = v_rcp_f32(d) (ray_inv), is within
+// 4.02u |q'| of the reference's fl(e / d), min and max keep a relative bound (|max a' -
+// max a| <= 4.05u max(|a|, |a'|)), so |lo' - lo| <= 8.2u |lo'| and the same for hi; the
+// test uses 16u plus an absolute floor.  Zero direction components are skipped through
 // the RayInv bias (see ray_inv); rays with a non-finite reciprocal (ri.exact) and
 // boxes near a tie take the exact reference test.
 // tlo (pruning) is a lower bound of the exact entry distance, -inf if undecided.
@@ -760,7 +760,7 @@ struct TraceParams {
     // heavy groups (hl_prev[0, *hc_prev)) run first and are skipped in the normal queues
     // (hf_prev); this frame records its own into the *_next buffers.  hs_* = summed group
     // durations (100 MHz ticks) for the threshold (4x the mean group).
-    int hist;
+    int hist, heavy_cap;      // heavy_cap: most heavy groups recorded per frame
     const int* hl_prev; int* hl_next;
     const unsigned char* hf_prev; unsigned char* hf_next;
     const unsigned long long* hctl_prev; unsigned long long* hctl_next;   // {count, sum}
@@ -816,6 +816,15 @@ __device__ __forceinline__ V4 hit_kd(const PT& P, const BvhRefs& bv, const Best&
 // Opaque to the optimiser: values derived from x (64-bit output addresses) are formed
 // here instead of being hoisted to the group start and spilled across the trace.
 __device__ __forceinline__ void opaque(int& x) { asm volatile("" : "+v"(x)); }
+// Build-defined sample offset k (rt_scene.cpp spp_offset: R2 sequence in double), computed
+// with the same correctly rounded double operations as the host table (no memory access in
+// the group loop: a vector load there waits, in order, for the previous group's stores and
+// for the work-ticket atomic in flight).
+__device__ __forceinline__ float2 spp_offset_dev(int k) {
+    const double u = (double)k * 0.7548776662466927, v = (double)k * 0.5698402909980532;
+    return make_float2((float)(u - floor(u)), (float)(v - floor(v)));
+}
+
 // A wave-uniform value made loop-variant where it is used: per-group constants derived from
 // it (camera terms of the kernel arguments) are recomputed there instead of being hoisted out
 // of the persistent group loop, held in VGPRs across the trace and spilled (the spill reloads
@@ -1179,8 +1188,11 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     int n_heavy = 0;
     unsigned long long thr = ~0ull, wave_sum = 0;
     if (P.hist) {
-        n_heavy = (int)P.hctl_prev[0];
-        if (P.hctl_prev[1]) thr = 4 * P.hctl_prev[1] / (unsigned long long)P.n_groups;
+        n_heavy = (int)min(P.hctl_prev[0], (unsigned long long)P.heavy_cap);
+        // heavy: over 4x the previous frame's mean group and over 20 us (2000 ticks of the 100 MHz
+        // clock) -- in a frame of uniformly cheap groups the mean-relative test alone flags
+        // timing noise, and a long heavy list (one atomic per group) is slower than none
+        if (P.hctl_prev[1]) thr = max(4 * P.hctl_prev[1] / (unsigned long long)P.n_groups, 2000ull);
     }
     int qi = n_heavy > 0 ? -1 : 0;                           // -1: the previous frame's heavy groups first
     // Lane 0 holds the raw result of the pending ticket request.  A ticket claims TPC
@@ -1194,7 +1206,13 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     auto step_of = [&](int q) { return q < 0 ? 1 : TPC; };
     auto request = [&](int q) {
         KTP& Pq = kparams();
-        if (lane == 0) pend = atomicAdd(q < 0 ? &Pq.work[16 * NQ] : &Pq.work[16 * ((q0 + q) % NQ)], step_of(q));
+        // The address goes through a VGPR so the atomic optimizer leaves the atomic alone:
+        // its rewrite waits for the returned value right after issuing it, while the value is
+        // needed only when the batch is used up (resolve), groups later.
+        unsigned long long a = (unsigned long long)(q < 0 ? &Pq.work[16 * NQ] : &Pq.work[16 * ((q0 + q) % NQ)]);
+        asm volatile("" : "+v"(a));
+        typedef __attribute__((address_space(1))) int gint;   // keep the global (not flat) atomic
+        if (lane == 0) pend = __hip_atomic_fetch_add((gint*)a, step_of(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         inflight = 1;
     };
     auto resolve = [&]() { inflight = 0; return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
@@ -1256,7 +1274,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             const bool act = valid && k < P.spp;
             Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
             if (act) {
-                const float2 o = P.spp_off[k];
+                const float2 o = spp_offset_dev(k);
 #if RT_EXP_NOCAM                                               // experiment: no camera ray
                 r0.d = v3((float)px + o.x, (float)py + o.y, 1.0f);
 #else
@@ -1357,8 +1375,13 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             const bool heavy = dur > thr;
             wave_sum += dur;
             if (lane_id_fresh() == 0) {
-            P.hf_next[g] = heavy ? 1 : 0;
-            if (heavy) P.hl_next[atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1)] = g;
+            // at most heavy_cap recorded (a few per wave: the list is there to start the frame's
+            // longest groups first); a group flagged in hf_next is always in hl_next
+            int slot = -1;
+            if (heavy) slot = atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1);
+            const bool rec = heavy && slot < P.heavy_cap;
+            P.hf_next[g] = rec ? 1 : 0;
+            if (rec) P.hl_next[slot] = g;
             if (P.gdur) {
                 P.gdur[g] = (unsigned)dur;
                 if (PROF) {                                    // wave step counts and cycle split of the group
@@ -2421,6 +2444,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const int waves_needed = P.n_groups;
     int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
+    P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     void* args[] = {&P, &S};
     HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, e0, e1, 0));
     HIPCHK(hipGetLastError());

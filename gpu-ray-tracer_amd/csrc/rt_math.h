@@ -269,9 +269,10 @@ RT_HD bool tri_hit(V3 a, V3 b, V3 c, V3 pn, float area, const Ray& r, float& tim
 // approximations with a rigorous error bound and return the reference's exact
 // answer whenever the approximation is decisive; inside the (tiny) uncertainty
 // band they run the exact reference arithmetic.  Derivation (u = 2^-24):
-//  * q' = fl(e * fl(1/d)) vs q = fl(e / d): |q' - q| <= 3.0001 u |e/d| in the
-//    normal range; the bound used is 16 u max|q'| + 2^-120 (absolute floor for
-//    the subnormal range; non-finite values always fall back).  min/max of
+//  * q' = fl(e * r'), r' = v_rcp_f32(d) within 1 ulp of 1/d, vs q = fl(e / d):
+//    |q' - q| <= 4.02 u |q'| in the normal range (ray_inv below); the bound used is
+//    16 u max|q'| + 2^-120 (absolute floor for the subnormal range; non-finite values
+//    always fall back).  min/max of
 //    perturbed values move by at most the same bound, and the slab test's
 //    early exits are monotone, so its outcome is (T_min <= T_max && T_max >= 1e-5)
 //    evaluated once at the end.
@@ -281,16 +282,30 @@ RT_HD bool tri_hit(V3 a, V3 b, V3 c, V3 pn, float area, const Ray& r, float& tim
 // b* = +inf for a zero direction component (the reference skips that slab): the packed
 // pair test forms q0 = fma(mn - o, inv, -b), q1 = fma(mx - o, inv, +b), i.e. (-inf, +inf)
 // = no constraint for a skipped axis and exactly fl((mn - o) * inv) otherwise.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+#else
+RT_HD float fast_sqrt(float x) { return sqrtf(x); }
+RT_HD float fast_rcp(float x) { return 1.0f / x; }
+#endif
+// The reciprocals are v_rcp_f32 on the device (within 1 ulp, i.e. 2u relative, for
+// 2^-64 <= |d| <= 2^64): a quotient q' = fl(e * r') is then within 4.02u |q'| of the
+// reference's fl(e / d) (2u + 1u + 1u and second-order terms), and the box filters' margins
+// are 16u per slab bound (min/max keep the relative bound; the sums below add < 1u each).
+// Components outside that range (never the case for the normalised directions of the
+// integrator, whose nonzero components are >= ~1e-7) take the exact reference test.
 struct RayInv { float ix, iy, iz, bx, by, bz; int exact; };
+RT_HD bool rcp_range(float d) { const float a = fabsf(d); return d == 0.0f || (a >= 0x1p-64f && a <= 0x1p64f); }
 RT_HD RayInv ray_inv(const Ray& r) {
     RayInv v;
-    v.ix = r.d.x != 0 ? rcp_cr(r.d.x) : 0.0f;
-    v.iy = r.d.y != 0 ? rcp_cr(r.d.y) : 0.0f;
-    v.iz = r.d.z != 0 ? rcp_cr(r.d.z) : 0.0f;
+    v.ix = r.d.x != 0 ? fast_rcp(r.d.x) : 0.0f;
+    v.iy = r.d.y != 0 ? fast_rcp(r.d.y) : 0.0f;
+    v.iz = r.d.z != 0 ? fast_rcp(r.d.z) : 0.0f;
     v.bx = r.d.x != 0 ? 0.0f : INFINITY;
     v.by = r.d.y != 0 ? 0.0f : INFINITY;
     v.bz = r.d.z != 0 ? 0.0f : INFINITY;
-    v.exact = !(isfinite(v.ix) && isfinite(v.iy) && isfinite(v.iz));   // subnormal components
+    v.exact = !(rcp_range(r.d.x) && rcp_range(r.d.y) && rcp_range(r.d.z));
     return v;
 }
 constexpr float FILT_BOX = 0x1p-20f;       // 16 u
@@ -331,13 +346,6 @@ RT_HD bool box_hit_ft(V3 mn, V3 mx, const Ray& r, const RayInv& ri, float& tlo) 
     return box_hit(mn, mx, r);
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-#else
-RT_HD float fast_sqrt(float x) { return sqrtf(x); }
-RT_HD float fast_rcp(float x) { return 1.0f / x; }
-#endif
 
 // tri_hit (above) + TriInner::tri_hit's acceptance (trimesh.cu:56), filtered.
 // inv_area = fl(1 / area) (host-precomputed; only used by the filter).
