@@ -260,22 +260,29 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
     const f2 hi = vmin(vmin(vmax(qx0, qx1), vmax(qy0, qy1)), vmax(qz0, qz1));
 #endif
 #if RT_FILTERED
-    const f2 el{fabsf(lo.x) * FILT_BOX + FILT_ABS, fabsf(lo.y) * FILT_BOX + FILT_ABS};
-    const f2 eh{fabsf(hi.x) * FILT_BOX + FILT_ABS, fabsf(hi.y) * FILT_BOX + FILT_ABS};
-    const f2 sep = (lo + el) - (hi - eh);                     // > 0 certainly lo > hi; <= 0 certainly lo <= hi
-    const f2 gap = (lo - el) - (hi + eh);
-    const f2 hlo = hi - eh, hhi = hi + eh;
+    // Certain outcomes (the exact reference result known): with el, eh the error margins of
+    // lo, hi, c = lo + el and a = hi - eh bound the reference's tmin from above and its tmax
+    // from below, so max(c, 1e-5) <= a is certainly a hit; with d = lo - el, b = hi + eh,
+    // max(d, 1e-5) > b is certainly a miss (bounding_box.cu:98: tmin > tmax || tmax < 1e-5).
+    // For filtered rays lo and hi are finite (ray_inv sends a direction without a nonzero
+    // component to the exact test), so the max forms equal the pairs of comparisons.
+    // Lanes in between run the exact reference test; one uniform branch for both children.
+    const f2 el{fmaf(fabsf(lo.x), FILT_BOX, FILT_ABS), fmaf(fabsf(lo.y), FILT_BOX, FILT_ABS)};
+    const f2 eh{fmaf(fabsf(hi.x), FILT_BOX, FILT_ABS), fmaf(fabsf(hi.y), FILT_BOX, FILT_ABS)};
+    const f2 cc = lo + el, aa = hi - eh, dd = lo - el, bb = hi + eh;
     const bool fx = active && !ri.exact;
-    // certainly a miss / certainly a hit (exact reference result known)
-    const bool m0 = !nd0 || (fx && (gap.x > 0.0f || hhi.x < THRESH));
-    const bool m1 = !nd1 || (fx && (gap.y > 0.0f || hhi.y < THRESH));
-    const bool c0 = fx && !m0 && sep.x <= 0.0f && hlo.x >= THRESH;
-    const bool c1 = fx && !m1 && sep.y <= 0.0f && hlo.y >= THRESH;
+    const bool c0 = fx && nd0 && fmaxf(cc.x, THRESH) <= aa.x;
+    const bool c1 = fx && nd1 && fmaxf(cc.y, THRESH) <= aa.y;
+    const bool m0 = !nd0 || (fx && fmaxf(dd.x, THRESH) > bb.x);
+    const bool m1 = !nd1 || (fx && fmaxf(dd.y, THRESH) > bb.y);
     h0 = c0; h1 = c1;
-    if (c0) t0 = lo.x - el.x;
-    if (c1) t1 = lo.y - el.y;
-    if (active && !m0 && !c0) h0 = exact(0);
-    if (active && !m1 && !c1) h1 = exact(1);
+    t0 = c0 ? dd.x : -INFINITY;
+    t1 = c1 ? dd.y : -INFINITY;
+    const bool x0 = active && !m0 && !c0, x1 = active && !m1 && !c1;
+    if (__builtin_expect(__ballot(x0 || x1) != 0, 0)) {
+        if (x0) h0 = exact(0);
+        if (x1) h1 = exact(1);
+    }
 #else
     h0 = active && nd0 && exact(0);
     h1 = active && nd1 && exact(1);
@@ -293,6 +300,25 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
+#ifndef RT_EXP_PAD
+#define RT_EXP_PAD 0         // experiment builds: sensitivity probe, RT_EXP_PAD dummy VALU at site RT_EXP_PAD_SITE
+#define RT_EXP_PAD_SITE 0
+#endif
+template <int SITE> __device__ __forceinline__ void exp_pad() {
+#if RT_EXP_PAD
+    if (SITE == RT_EXP_PAD_SITE) {
+        int x = 0;
+#pragma unroll
+#if RT_EXP_PAD_SALU
+        for (int i = 0; i < RT_EXP_PAD; i++) asm volatile("s_add_u32 %0, 1, %0" : "+s"(x));
+        asm volatile("" :: "s"(x));
+#else
+        for (int i = 0; i < RT_EXP_PAD; i++) asm volatile("v_add_u32 %0, 1, %0" : "+v"(x));
+        asm volatile("" :: "v"(x));
+#endif
+    }
+#endif
+}
 
 __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
     const float4 I = bv.inst[ti];
@@ -565,6 +591,9 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // an iteration tests a node's pair -- or, for a popped pending leaf B, re-tests its
         // parent's pair for child B only -- then runs at most one leaf; when both children
         // are leaves, B waits in registers (h2, t2, inst2) for the next iteration.
+        // the pruning cut changes only when a leaf improves the closest hit: kept, and
+        // recomputed after each leaf visit instead of at every step
+        float ct = prune ? cut() : INFINITY;
         int node = 0, sp = 0, stk = 0, bonly = 0, has2 = 0, inst2 = 0;
         bool h2 = false;
         float t2 = 0.0f;
@@ -575,23 +604,21 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             float ltl = 0.0f;
             int linst = -1;                                    // leaf of this iteration (uniform), -1: none
             if (has2) {                                        // leaf B right after leaf A (fresh cut)
-                lh = h2 && !(prune && t2 > cut());
+                lh = h2 && !(t2 > ct);
                 ltl = t2; linst = inst2; has2 = 0;
             } else {
                 const float4* rec = bv.fnode + 4 * node;
                 bool h0, h1;
                 float t0, t1;
                 if (PROF) wc.wpair++;
+                exp_pad<1>();                                  // experiment: per child-pair step
                 // child references first, in the same LDS batch as the boxes: one round trip
                 // per step (read after the pair test, they cost a second dependent one)
                 const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
                 const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
                 pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
-                if (prune) {
-                    const float ct = cut();
-                    h0 = h0 && !(t0 > ct);
-                    h1 = h1 && !(t1 > ct);
-                }
+                h0 = h0 && !(t0 > ct);                         // (ct = +inf without pruning)
+                h1 = h1 && !(t1 > ct);
                 const int bo = bonly;                          // child B only (popped leaf B)
                 bonly = 0;
                 const bool goA = !bo && ra >= 0 && __ballot(h0) != 0;
@@ -617,6 +644,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 }
             }
             if (linst >= 0 && __ballot(lh)) {
+                exp_pad<2>();                                  // experiment: per leaf visit
                 if (!pre_ok) {
                     if (AXIS) pre = dir_pre<true>(r.d);        // S.tri_ax set: identity rotations
                     else if (S.ident_all) pre = dir_pre(r.d);
@@ -628,6 +656,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                     hit = true;
                     if (b.time <= occl_t) active = false;
                 }
+                if (prune) ct = cut();
                 if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
                 if (!__ballot(active)) break;                  // every lane occluded
             }
@@ -1013,6 +1042,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             dtl.x = get(); dtl.y = get(); dtl.z = get();
         }
         unsigned long long c1 = 0;
+        exp_pad<3>();                                          // experiment: per query
         if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
         if (!need) continue;
         int hmat = 0;
@@ -1254,6 +1284,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
+        exp_pad<4>();                                          // experiment: per group
         const int ln = lane_id_fresh();
         const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
         const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;

@@ -305,7 +305,8 @@ RT_HD RayInv ray_inv(const Ray& r) {
     v.bx = r.d.x != 0 ? 0.0f : INFINITY;
     v.by = r.d.y != 0 ? 0.0f : INFINITY;
     v.bz = r.d.z != 0 ? 0.0f : INFINITY;
-    v.exact = !(rcp_range(r.d.x) && rcp_range(r.d.y) && rcp_range(r.d.z));
+    v.exact = !(rcp_range(r.d.x) && rcp_range(r.d.y) && rcp_range(r.d.z)) ||
+              (r.d.x == 0.0f && r.d.y == 0.0f && r.d.z == 0.0f);    // no slab constrains t
     return v;
 }
 constexpr float FILT_BOX = 0x1p-20f;       // 16 u

@@ -240,3 +240,38 @@ def test_timed_frames(gpu):
     one = s.timing_collect()
     assert one["frames"] == 1 and one["bvh_ms_total"] < 0.01 and one["trace_ms_total"] > 0
     assert s.timing_collect()["frames"] == 0
+
+
+@pytest.mark.parametrize("spp", [8, 3])
+def test_fast_kernel_exact_spp8_sky_and_horizon(gpu, spp):
+    """The bench's sample mapping (8 samples per pixel: one-round-trip exchange, clamp before
+    the exchange) and the whole-group miss test: fast frames == counted frames bit for bit
+    with the camera at the scene's pose, turned to the sky (every group a miss group), at
+    the horizon (groups straddling it) and from random poses; with every output, and with
+    the colour alone (the raw-sum exchange skipped).  spp = 3 takes the generic exchange."""
+    import torch
+    w, h = 240, 160
+    s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    pos0, q0 = s.camera()
+    rng = np.random.default_rng(77)
+    poses = [(pos0, q0), (pos0, (-0.3826834, 0.0, 0.0, 0.9238795)), (pos0, (0.0, 0.0, 0.0, 1.0)),
+             ((0.5, 3.0, -12.0), (0.0, 0.0, 0.0, 1.0))]
+    for _ in range(3):
+        q = rng.normal(size=4)
+        poses.append(([float(rng.uniform(-6, 6)), float(rng.uniform(0, 12)), float(rng.uniform(-9, 9))],
+                      [float(x) for x in q / np.linalg.norm(q)]))
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    sky_seen = lit_seen = False
+    buf = torch.zeros((h, w), dtype=torch.int32, device="cuda")
+    for pos, q in poses:
+        s.set_camera(pos, q)
+        full = s.render(spp=spp, want=want, stats=True)
+        fast = s.render(spp=spp, want=want, stats=False)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, q, k)
+        s.render_device(spp=spp, rgba_ptr=buf.data_ptr(), compact=False, sync=True)
+        assert np.array_equal(buf.cpu().numpy().view(np.uint32), full["rgba"]), (pos, q)
+        hit = full["hit_inst"] >= 0
+        sky_seen |= bool((~hit).all())
+        lit_seen |= bool(hit.any() and (~hit).any())
+    assert sky_seen and lit_seen
