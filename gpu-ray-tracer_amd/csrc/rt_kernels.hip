@@ -591,21 +591,23 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // an iteration tests a node's pair -- or, for a popped pending leaf B, re-tests its
         // parent's pair for child B only -- then runs at most one leaf; when both children
         // are leaves, B waits in registers (h2, t2, inst2) for the next iteration.
-        // the pruning cut changes only when a leaf improves the closest hit: kept, and
-        // recomputed after each leaf visit instead of at every step
-        float ct = prune ? cut() : INFINITY;
+        // Per-lane state as floats, not booleans (a boolean live across the loop's blocks
+        // costs scalar mask updates on every edge): a child's test result is its entry bound
+        // t, or NaN for a miss; the lane's cut ct (the pruning bound, +inf without pruning)
+        // is NaN once the lane is inactive (no query, or occluded), so "hit and not pruned"
+        // is the one comparison t <= ct, false for every NaN.  The cut changes only when a
+        // leaf improves the closest hit: recomputed after each leaf visit, not every step.
+        const float QNAN = __builtin_nanf("");
+        float ct = !active_in ? QNAN : prune ? cut() : INFINITY;
         int node = 0, sp = 0, stk = 0, bonly = 0, has2 = 0, inst2 = 0;
-        bool h2 = false;
-        float t2 = 0.0f;
+        float t2 = QNAN;
         const int my_lane = __lane_id();
         auto push = [&](int e) { stk = my_lane == sp ? e : stk; sp++; };   // v_writelane
         for (;;) {
-            bool lh = false;
-            float ltl = 0.0f;
-            int linst = -1;                                    // leaf of this iteration (uniform), -1: none
-            if (has2) {                                        // leaf B right after leaf A (fresh cut)
-                lh = h2 && !(t2 > ct);
-                ltl = t2; linst = inst2; has2 = 0;
+            float lt = QNAN;                                   // leaf of this iteration: entry bound / NaN
+            int linst = -1;                                    // its instance (uniform), -1: none
+            if (has2) {                                        // leaf B right after leaf A (fresh cut below)
+                lt = t2; linst = inst2; has2 = 0;
             } else {
                 const float4* rec = bv.fnode + 4 * node;
                 bool h0, h1;
@@ -616,21 +618,21 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 // per step (read after the pair test, they cost a second dependent one)
                 const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
                 const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
-                pair_hit_at(rec, r, ri, active, h0, h1, t0, t1);
-                h0 = h0 && !(t0 > ct);                         // (ct = +inf without pruning)
-                h1 = h1 && !(t1 > ct);
+                pair_hit_at(rec, r, ri, ct == ct, h0, h1, t0, t1);
+                const float ta = h0 ? t0 : QNAN, tb = h1 ? t1 : QNAN;
+                const bool bA = __ballot(ta <= ct) != 0, bB = __ballot(tb <= ct) != 0;
                 const int bo = bonly;                          // child B only (popped leaf B)
                 bonly = 0;
-                const bool goA = !bo && ra >= 0 && __ballot(h0) != 0;
-                const bool goB = rb >= 0 && __ballot(h1) != 0;
-                if (!bo && ra < 0) { lh = h0; ltl = t0; linst = -1 - ra; }
+                const bool goA = !bo && ra >= 0 && bA;
+                const bool goB = rb >= 0 && bB;
+                if (!bo && ra < 0) { lt = ta; linst = -1 - ra; }
                 if (rb < 0) {
                     if (goA) {
-                        if (__ballot(h1)) push(-2 - node);
+                        if (bB) push(-2 - node);
                     } else if (linst >= 0) {
-                        h2 = h1; t2 = t1; inst2 = -1 - rb; has2 = 1;
+                        t2 = tb; inst2 = -1 - rb; has2 = 1;
                     } else {
-                        lh = h1; ltl = t1; linst = -1 - rb;
+                        lt = tb; linst = -1 - rb;
                     }
                 }
                 if (goA) {
@@ -643,6 +645,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                     push(rb);                                  // internal B after leaf A
                 }
             }
+            const bool lh = lt <= ct;                          // (ct only decreases: a fresh cut for leaf B)
             if (linst >= 0 && __ballot(lh)) {
                 exp_pad<2>();                                  // experiment: per leaf visit
                 if (!pre_ok) {
@@ -652,13 +655,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 }
                 const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
                 if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
-                if (lh && cast_local<false, AXIS, PROF>(S, bv, uni(linst), r, b, pre, wc, t_low(ltl))) {
-                    hit = true;
-                    if (b.time <= occl_t) active = false;
-                }
-                if (prune) ct = cut();
+                if (lh && cast_local<false, AXIS, PROF>(S, bv, uni(linst), r, b, pre, wc, t_low(lt)))
+                    if (b.time <= occl_t) ct = QNAN;           // occluded: this lane is done
+                if (prune && ct == ct) ct = cut();
                 if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
-                if (!__ballot(active)) break;                  // every lane occluded
+                if (!__ballot(ct == ct)) break;                // every lane occluded
             }
             if (has2) continue;
             if (sp == 0) break;
@@ -667,7 +668,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             if (e < 0) { node = -2 - e; bonly = 1; }
             else node = e;
         }
-        return hit;
+        return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
     }
     if (STATS) wc.nodes += __popcll(am);                       // root test
     bool hr, hdummy;
