@@ -288,6 +288,45 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
     h1 = active && nd1 && exact(1);
 #endif
 }
+// pair_hit_at for the fast traversal, with each child's result as one float: the entry
+// lower bound (lo - el, or -inf after the exact test) for a hit, NaN for a miss.  Certain
+// outcomes and the exact fallback as in pair_hit_at; the filtered-ray condition is folded
+// into the masks so no boolean is materialised.
+__device__ __forceinline__ void pair_hit_tt(const float4* rec, const Ray& r, const RayInv& ri, bool active,
+                                            float& ta, float& tb) {
+    const float4 A = rec[0], B = rec[1], C = rec[2];
+    const bool nd0 = A.x <= B.z, nd1 = A.y <= B.w;            // nondegenerate (bounding_box.cu:63-65)
+#if !RT_FILTERED
+    ta = active && nd0 && box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : __builtin_nanf("");
+    tb = active && nd1 && box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : __builtin_nanf("");
+    return;
+#endif
+    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
+        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
+        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
+        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
+        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
+        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
+    };
+    float lo0, hi0, lo1, hi1;
+    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
+    const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS);
+    const float el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
+    const float d0 = lo0 - el0, d1 = lo1 - el1;
+    const bool hc0 = fmaxf(lo0 + el0, THRESH) <= hi0 - eh0, hc1 = fmaxf(lo1 + el1, THRESH) <= hi1 - eh1;
+    const bool mc0 = fmaxf(d0, THRESH) > hi0 + eh0, mc1 = fmaxf(d1, THRESH) > hi1 + eh1;
+    const bool fx = active && !ri.exact;
+    const float QNAN = __builtin_nanf("");
+    ta = (fx && nd0 && hc0) ? d0 : QNAN;
+    tb = (fx && nd1 && hc1) ? d1 : QNAN;
+    const bool x0 = active && nd0 && (ri.exact || !(hc0 || mc0));
+    const bool x1 = active && nd1 && (ri.exact || !(hc1 || mc1));
+    if (__builtin_expect(__ballot(x0 || x1) != 0, 0)) {
+        if (x0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
+        if (x1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
+    }
+}
 __device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
                                          bool& h0, bool& h1, float& t0, float& t1) {
     pair_hit_at(np + 3 * k, r, ri, active, h0, h1, t0, t1);
@@ -610,16 +649,14 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 lt = t2; linst = inst2; has2 = 0;
             } else {
                 const float4* rec = bv.fnode + 4 * node;
-                bool h0, h1;
-                float t0, t1;
                 if (PROF) wc.wpair++;
                 exp_pad<1>();                                  // experiment: per child-pair step
                 // child references first, in the same LDS batch as the boxes: one round trip
                 // per step (read after the pair test, they cost a second dependent one)
                 const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
                 const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
-                pair_hit_at(rec, r, ri, ct == ct, h0, h1, t0, t1);
-                const float ta = h0 ? t0 : QNAN, tb = h1 ? t1 : QNAN;
+                float ta, tb;
+                pair_hit_tt(rec, r, ri, ct == ct, ta, tb);
                 const bool bA = __ballot(ta <= ct) != 0, bB = __ballot(tb <= ct) != 0;
                 const int bo = bonly;                          // child B only (popped leaf B)
                 bonly = 0;
