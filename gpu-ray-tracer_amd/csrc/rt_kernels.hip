@@ -194,6 +194,24 @@ struct BvhRefs {
 #ifndef RT_EXP_NOHIST
 #define RT_EXP_NOHIST 0
 #endif
+#ifndef RT_EXP_NOCHECK
+#define RT_EXP_NOCHECK 0     // experiment: heavy groups not skipped in the normal queues (run twice)
+#endif
+#ifndef RT_HIST_GROUPS_PER_WAVE
+#define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
+#endif
+#ifndef RT_EXP_NOTIME
+#define RT_EXP_NOTIME 0      // experiment: no clock reads for the history (every group light)
+#endif
+#ifndef RT_EXP_NOSTORE
+#define RT_EXP_NOSTORE 0     // experiment: flags stored for heavy groups only (stale flags stay)
+#endif
+#ifndef RT_EXP_MEMTIME
+#define RT_EXP_MEMTIME 0     // experiment: history clock = s_memtime (shader clock) instead of the RTC
+#endif
+#ifndef RT_EXP_NOREC
+#define RT_EXP_NOREC 0       // experiment: no duration recording (the history stays the first frame's)
+#endif
 #ifndef RT_FILTERED
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
@@ -1260,7 +1278,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         // heavy: over 4x the previous frame's mean group and over 20 us (2000 ticks of the 100 MHz
         // clock) -- in a frame of uniformly cheap groups the mean-relative test alone flags
         // timing noise, and a long heavy list (one atomic per group) is slower than none
-        if (P.hctl_prev[1]) thr = max(4 * P.hctl_prev[1] / (unsigned long long)P.n_groups, 2000ull);
+        if (P.hctl_prev[1]) thr = max(4 * P.hctl_prev[1] / (unsigned long long)P.n_groups, (RT_EXP_MEMTIME && !PROF) ? 40000ull : 2000ull);
     }
     int qi = n_heavy > 0 ? -1 : 0;                           // -1: the previous frame's heavy groups first
     // Lane 0 holds the raw result of the pending ticket request.  A ticket claims TPC
@@ -1316,9 +1334,10 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const int g = qi < 0 ? ldc(P.hl_prev, ticket)
                              : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)umod((unsigned)ticket * (unsigned)P.scramble)
                                                                          : (int)(((long long)ticket * P.scramble) % per_q));
-        if (g >= P.n_groups || (qi >= 0 && P.hist && ((ldc(reinterpret_cast<const uint32_t*>(P.hf_prev), g >> 2) >> (8 * (g & 3))) & 0xffu)))
+        if (g >= P.n_groups || (!RT_EXP_NOCHECK && qi >= 0 && P.hist && ((ldc(reinterpret_cast<const uint32_t*>(P.hf_prev), g >> 2) >> (8 * (g & 3))) & 0xffu)))
             continue;
-        const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
+        auto hclock = [&]() { return (RT_EXP_MEMTIME && !PROF) ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime(); };
+        const unsigned long long g_start = P.hist && !RT_EXP_NOTIME ? hclock() : 0;
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
@@ -1438,9 +1457,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
-        if (kparams().hist) {                                  // record for the next frame's order
+        if (!RT_EXP_NOREC && kparams().hist) {                 // record for the next frame's order
             KTP& P = kparams();
-            const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;   // wave-uniform (scalar)
+            const unsigned long long dur = RT_EXP_NOTIME ? 0 : hclock() - g_start;   // wave-uniform (scalar)
             const bool heavy = dur > thr;
             wave_sum += dur;
             if (lane_id_fresh() == 0) {
@@ -1449,7 +1468,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             int slot = -1;
             if (heavy) slot = atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1);
             const bool rec = heavy && slot < P.heavy_cap;
-            P.hf_next[g] = rec ? 1 : 0;
+            if (!RT_EXP_NOSTORE || rec) P.hf_next[g] = rec ? 1 : 0;
             if (rec) P.hl_next[slot] = g;
             if (P.gdur) {
                 P.gdur[g] = (unsigned)dur;
@@ -2438,22 +2457,6 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * (NQ + 1) * sizeof(int), st));
-    // longest-first history (fast frames): valid while the launch layout is unchanged
-    P.hist = 0;
-    if (!want_stats && !dbg && !RT_EXP_NOHIST) {
-        const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
-        int r;
-        if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
-        const int prev = s->hist_parity, next = 1 - prev;
-        P.hist = 1;
-        P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
-        P.hf_prev = s->d_hflag[prev]; P.hf_next = s->d_hflag[next];
-        P.hctl_prev = s->d_hctl + 2 * prev; P.hctl_next = s->d_hctl + 2 * next;
-        if (s->hctl_zeroed != next) HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
-        s->hist_parity = next;
-    }
-    s->work_zeroed = false;                                   // this launch consumes the counters
-    s->hctl_zeroed = -1;
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     const bool ft = mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
@@ -2514,6 +2517,28 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
     P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
+    // longest-first history (fast frames): valid while the launch layout is unchanged
+    // Only where a wave runs few groups (1080p 8-way row slices: ~8 per wave): with more (63
+    // for a whole 1080p frame, 16 for a 4-way slice) the dynamic queues already balance the
+    // frame and the two clock reads per group cost as much as the shorter tail saves or more
+    // (measured, four frames in flight, ms per frame with / without: whole frame 0.919 / 0.914,
+    // 4-way 0.360 / 0.360, 8-way 0.179-0.186 / 0.200-0.204; profiles/r02/hist_policy.log).
+    P.hist = 0;
+    const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
+    if (!want_stats && !dbg && !RT_EXP_NOHIST && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
+        const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
+        int r;
+        if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
+        const int prev = s->hist_parity, next = 1 - prev;
+        P.hist = 1;
+        P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
+        P.hf_prev = s->d_hflag[prev]; P.hf_next = s->d_hflag[next];
+        P.hctl_prev = s->d_hctl + 2 * prev; P.hctl_next = s->d_hctl + 2 * next;
+        if (s->hctl_zeroed != next) HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
+        s->hist_parity = next;
+    }
+    s->work_zeroed = false;                                   // this launch consumes the counters
+    s->hctl_zeroed = -1;
     void* args[] = {&P, &S};
     HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, e0, e1, 0));
     HIPCHK(hipGetLastError());
