@@ -61,6 +61,9 @@ constexpr int PARK_LDS_LIMIT = 158 * 1024;   // BVH image + parking area (160 KB
 #define RT_NQ 8
 #endif
 constexpr int NQ = RT_NQ;                    // work queues (one per XCD dispatch slot), 64-B apart
+// work counters: [16 q] queue q's tickets, [16 NQ] the heavy list's, [16 (NQ + 1 + q)] the
+// length of live-group list q (sky_kernel)
+constexpr int WORK_INTS = 16 * (2 * NQ + 1);
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -196,6 +199,15 @@ struct BvhRefs {
 #endif
 #ifndef RT_EXP_NOCHECK
 #define RT_EXP_NOCHECK 0     // experiment: heavy groups not skipped in the normal queues (run twice)
+#endif
+#ifndef RT_EXP_SKYCMP
+#define RT_EXP_SKYCMP 0      // experiment: trace kernel runs its own sky test and marks disagreements
+#endif
+#ifndef RT_EXP_GLC
+#define RT_EXP_GLC 0
+#endif
+#ifndef RT_SKY_PREPASS
+#define RT_SKY_PREPASS 1     // sky groups decided and written by sky_kernel before the trace kernel
 #endif
 #ifndef RT_HIST_GROUPS_PER_WAVE
 #define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
@@ -855,6 +867,13 @@ struct TraceParams {
     int* dbg_log;             // debug_cast event log (NULL in normal frames)
     int dbg_x, dbg_y;
     unsigned* gdur;           // profiling (rt_profile_groups): per-group duration, 100 MHz ticks; NULL normally
+    // Sky pre-pass (sky_kernel, fast frames): gsky[g] = 1 when no primary of group g enters
+    // the tree's root -- its outputs are written already and the trace kernel skips it.
+    // NULL: no pre-pass (the trace kernel runs the same test itself).
+    const unsigned char* gsky;
+    // Live-group lists (sky_kernel): queue q's groups are live[q * live_cap + i] for i below
+    // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
+    const int* live; int live_cap;
 };
 
 // The launch's TraceParams read in place from the kernel-argument segment (constant address
@@ -1290,6 +1309,11 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     // loop without tracing).
     int pend = 0, inflight = 0;
     auto step_of = [&](int q) { return q < 0 ? 1 : TPC; };
+    // live lists: tickets [0, 2^k) of a list of n <= 2^k groups visit (t * odd) mod 2^k, a
+    // bijection that spreads consecutive tickets over the list (arrival order is roughly
+    // raster order, where expensive regions cluster); indices >= n are skipped
+    auto live_n = [&](int q) { return ldc(kparams().work, 16 * (NQ + 1 + (q0 + q) % NQ)); };
+    auto live_span = [&](int q) { const int n = live_n(q); return n <= 1 ? n : 1 << (32 - __builtin_clz((unsigned)n - 1)); };
     auto request = [&](int q) {
         KTP& Pq = kparams();
         // The address goes through a VGPR so the atomic optimizer leaves the atomic alone:
@@ -1310,7 +1334,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         KTP& P = kparams();                                    // this group's reads of the launch parameters
         for (;;) {                                             // next work index tbase + j of queue qi
             if (qi >= NQ) break;
-            const int lim = qi < 0 ? n_heavy : per_q;
+            const int lim = qi < 0 ? n_heavy : kparams().live ? live_span(qi) : per_q;
             if (tbase + j >= lim) {                             // queue drained (a pending batch is past it too)
                 if (inflight) (void)resolve();
                 qi++; j = 0;
@@ -1331,10 +1355,27 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         // The scheduling history is read with scalar loads: a vector load here would wait
         // (vmcnt is in order) for the previous group's output stores to be acknowledged.
         auto umod = [&](unsigned n) { return n - udiv(n, kld(P.div_perq)) * (unsigned)per_q; };
+        auto live_g = [&]() {
+            const int n = live_n(qi);
+            const int i = (int)(((unsigned)ticket * 0x9E3779B1u) & (unsigned)(live_span(qi) - 1));
+            return i < n ? ldc(P.live, ((q0 + qi) % NQ) * P.live_cap + i) : P.n_groups;
+        };
         const int g = qi < 0 ? ldc(P.hl_prev, ticket)
+                             : P.live ? live_g()
                              : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)umod((unsigned)ticket * (unsigned)P.scramble)
                                                                          : (int)(((long long)ticket * P.scramble) % per_q));
-        if (g >= P.n_groups || (!RT_EXP_NOCHECK && qi >= 0 && P.hist && ((ldc(reinterpret_cast<const uint32_t*>(P.hf_prev), g >> 2) >> (8 * (g & 3))) & 0xffu)))
+#if RT_EXP_GLC
+        auto flag = [&](const unsigned char* f) {
+            uint32_t v;
+            const uint32_t* a = reinterpret_cast<const uint32_t*>(f) + (g >> 2);
+            asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
+            return (v >> (8 * (g & 3))) & 0xffu;
+        };
+#else
+        auto flag = [&](const unsigned char* f) { return (ldc(reinterpret_cast<const uint32_t*>(f), g >> 2) >> (8 * (g & 3))) & 0xffu; };
+#endif
+        if (g >= P.n_groups || (qi < 0 && P.gsky && !RT_EXP_SKYCMP && flag(P.gsky)) ||    // sky group: done by sky_kernel
+            (!RT_EXP_NOCHECK && qi >= 0 && P.hist && flag(P.hf_prev)))
             continue;
         auto hclock = [&]() { return (RT_EXP_MEMTIME && !PROF) ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime(); };
         const unsigned long long g_start = P.hist && !RT_EXP_NOTIME ? hclock() : 0;
@@ -1352,6 +1393,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const int py = P.row0 + pr * P.row_step;
         const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
         const bool me = valid && sub_g == 0 && px == P.dbg_x && py == P.dbg_y;
+        const int skyflag = (RT_EXP_SKYCMP && P.gsky) ? (int)flag(P.gsky) : -1;
+        int skybad = 0;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
@@ -1376,7 +1419,8 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // tree's root -- the traversal's first step, same test -- every sample misses, its
             // radiance is the integrator's initial zero (scene.cu:124-126) and the group's
             // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
-            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && !__ballot(ft_root_hit(S, bv, act, r0))) {
+            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && (RT_EXP_SKYCMP || !kparams().gsky) && !__ballot(ft_root_hit(S, bv, act, r0))) {
+                if (skyflag == 0) skybad = 1;
                 if (act && k == 0) {
                     int op = pix_index;
                     opaque(op);
@@ -1385,6 +1429,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                 }
                 break;                                         // sum_c = sum_r = 0
             }
+            if (skyflag == 1) skybad = 2;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
 #if RT_EXP_NOTRACE                                             // experiment: group overhead only
             V4 c = v4(r0.d.x, r0.d.y, r0.d.z, 1.0f);
@@ -1450,7 +1495,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
             const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
                                  ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
-            if (P.rgba) P.rgba[p] = enc;
+            if (P.rgba) P.rgba[p] = (RT_EXP_SKYCMP && skybad) ? 0xDEAD0000u + (unsigned)skybad : enc;
             if (P.radiance) P.radiance[p] = make_float4(mean(sum_r.x), mean(sum_r.y), mean(sum_r.z), mean(sum_r.w));
         }
         if (STATS && P.stats && lane == 0) {                 // profiling: heaviest group (PROF: rt_profile_groups)
@@ -1505,6 +1550,68 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     }
 }
 
+
+// Sky pre-pass of the fast frames: one wave per pixel group, the trace kernel's lane mapping
+// (lane = pixel x sample), the primary ray of each lane (camera_at, camera.cu:33-42) and the
+// traversal's first step on it (ft_root_hit: the same ray_inv, zero-axis cut and pair test on
+// the root's children as closest_hit's first iteration).  A group none of whose primaries
+// enters the root is a sky group: every sample's query returns no hit, its radiance is the
+// integrator's initial zero (scene.cu:124-126), so the group's outputs are written here --
+// rgba = the encoding of a zero mean (0), radiance 0, hit ids -1 -- exactly what the trace
+// kernel's own whole-group miss test writes, and gsky[g] = 1 tells the trace kernel to skip
+// the group.  84% of world8_stress's 1080p groups are sky: in the persistent trace kernel
+// each one cost the group loop's whole prologue (ticket, parameter loads, register spills
+// and restores around the integrator) -- a lean, high-occupancy kernel does the test
+// instead.  The root records are read from global memory (all lanes the same address).
+__global__ __launch_bounds__(1024) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
+    __shared__ int s_cnt, s_base;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, L = P.lanes_per_px;
+    const int g = blockIdx.x * 16 + wv;                        // 16 groups per block, one per wave
+    if (threadIdx.x == 0) s_cnt = 0;
+    bool sky = true;
+    if (g < P.n_groups) {                                      // whole waves
+        const int gy = g / P.n_gx, gx = g - gy * P.n_gx;
+        const int pix_g = lane / L, sub_g = lane - pix_g * L;
+        const int px = gx * P.gw + pix_g % P.gw, pr = gy * P.gh + pix_g / P.gw;
+        const bool valid = pix_g < P.px_per_wave && px < P.W && pr < P.n_rows;
+        const int py = P.row0 + pr * P.row_step;
+        const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;
+        const bool act = valid && sub_g < P.spp;               // k = sub_g (spp <= 64: one round)
+        Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
+        if (act) {
+            const float2 o = spp_offset_dev(sub_g);
+            r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
+        }
+        BvhRefs bv{};
+        bv.fnode = S.fnode;
+        sky = __ballot(ft_root_hit(S, bv, act, r0)) == 0;
+        if (lane == 0) {
+            gsky[g] = sky ? 1 : 0;
+            // the trace kernel records (hf_next) only the groups it runs: a sky group's entry
+            // must not keep a heavy flag from the frame that last wrote this buffer
+            if (sky && P.hist) P.hf_next[g] = 0;
+        }
+        if (sky && !RT_EXP_SKYCMP) {
+            if (act && sub_g == 0) {
+                if (P.hit_inst) P.hit_inst[pix_index] = -1;
+                if (P.hit_tri) P.hit_tri[pix_index] = -1;
+            }
+            if (valid && sub_g == 0) {
+                if (P.rgba) P.rgba[pix_index] = 0u;           // to_encoding of Color(0, 0, 0, 0)
+                if (P.radiance) P.radiance[pix_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
+        }
+    }
+    // live groups appended to list (block % NQ): one global atomic per block
+    __syncthreads();
+    int slot = 0;
+    if (!sky && lane == 0) slot = atomicAdd(&s_cnt, 1);
+    __syncthreads();
+    const int q = blockIdx.x % NQ;
+    if (threadIdx.x == 0 && s_cnt > 0) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], s_cnt);
+    __syncthreads();
+    if (!sky && lane == 0) live[q * P.live_cap + s_base + slot] = g;
+}
 
 // Experiment kernel (profiling aid, not on the product path): closest hit of the
 // primary rays only, persistent blocks with the BVH in LDS, one sample per lane.
@@ -1927,6 +2034,8 @@ struct rt_scene {
     int hist_cap = 0, hist_parity = 0;
     int hctl_zeroed = -1;                        // heavy-list slot the pending bvh_build_kernel zeroes (-1: none)
     long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    unsigned char* d_gsky = nullptr; int gsky_cap = 0;   // sky pre-pass flags (TraceParams::gsky)
+    int* d_live = nullptr; int live_cap = 0;             // sky pre-pass live-group lists [NQ][live_cap]
     float2* d_spp = nullptr; int spp_cap = 0;
     unsigned long long* d_stats = nullptr;
     uint32_t* d_canvas = nullptr;
@@ -1959,6 +2068,8 @@ struct rt_scene {
         unsigned long long* d_hctl = nullptr;
         int hist_cap = 0, hist_parity = 0, hctl_zeroed = -1;
         long long hist_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+        unsigned char* d_gsky = nullptr; int gsky_cap = 0;
+        int* d_live = nullptr; int live_cap = 0;
         DInst* d_insts = nullptr; float4* d_inst4 = nullptr;
         DInst* h_insts_pin = nullptr; float4* h_inst4_pin = nullptr;
         unsigned slot_inst_gen = 0;
@@ -1983,6 +2094,7 @@ void select_slot(rt_scene* s, int i) {
         f(s->d_hctl, o.d_hctl); f(s->hist_cap, o.hist_cap); f(s->hist_parity, o.hist_parity);
         f(s->hctl_zeroed, o.hctl_zeroed);
         for (int k = 0; k < 8; k++) f(s->hist_key[k], o.hist_key[k]);
+        f(s->d_gsky, o.d_gsky); f(s->gsky_cap, o.gsky_cap); f(s->d_live, o.d_live); f(s->live_cap, o.live_cap);
         f(s->d_insts, o.d_insts); f(s->d_inst4, o.d_inst4);
         f(s->h_insts_pin, o.h_insts_pin); f(s->h_inst4_pin, o.h_inst4_pin);
         f(s->slot_inst_gen, o.slot_inst_gen);
@@ -2171,7 +2283,7 @@ int upload(rt_scene* s) {
     HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
-    HIPCHK(hipMalloc((void**)&s->d_work, 16 * (NQ + 1) * sizeof(int)));
+    HIPCHK(hipMalloc((void**)&s->d_work, WORK_INTS * sizeof(int)));
     if ((r = upload_inst4(s)) != RT_OK) return r;
     if ((r = up(s->d_tri_ax, tri_axis_records(h))) != RT_OK) return r;
     if ((r = up(s->d_mesh_box, mesh_boxes(h))) != RT_OK) return r;
@@ -2261,7 +2373,7 @@ int ensure_other_slot(rt_scene* s) {
         HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
         HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
-        HIPCHK(hipMalloc((void**)&o.d_work, 16 * (NQ + 1) * sizeof(int)));
+        HIPCHK(hipMalloc((void**)&o.d_work, WORK_INTS * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_insts, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(DInst)));
         HIPCHK(hipMalloc((void**)&o.d_inst4, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(float4)));
         o.slot_inst_gen = 0;                                 // filled by sync_slot_insts on first use
@@ -2349,7 +2461,7 @@ int build_bvh(rt_scene* s, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e
     A.tree = s->d_tree;
     A.node_pair = reinterpret_cast<float*>(s->d_node_pair); A.leaf_inst = s->d_leaf;
     A.fnode = s->d_fnode; A.n_real = s->n_real;
-    A.work = s->d_work; A.n_work = 16 * (NQ + 1);
+    A.work = s->d_work; A.n_work = WORK_INTS;
     // the slot the next fast frame records its heavy list into (launch_trace skips its memset)
     A.hctl = s->d_hctl ? s->d_hctl + 2 * (1 - s->hist_parity) : nullptr;
     s->hctl_zeroed = s->d_hctl ? 1 - s->hist_parity : -1;
@@ -2456,7 +2568,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
     P.work = s->d_work;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
-    if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, 16 * (NQ + 1) * sizeof(int), st));
+    if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, WORK_INTS * sizeof(int), st));
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     const bool ft = mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
@@ -2539,8 +2651,29 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     }
     s->work_zeroed = false;                                   // this launch consumes the counters
     s->hctl_zeroed = -1;
+    // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
+    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0 && RT_SKY_PREPASS;
+    if (sky) {
+        if (P.n_groups > s->gsky_cap) {
+            dfree(s->d_gsky);
+            const int cap = (std::max(P.n_groups, 1024) + 3) & ~3;   // whole dwords (scalar loads)
+            HIPCHK(hipMalloc((void**)&s->d_gsky, cap));
+            s->gsky_cap = cap;
+        }
+        const int sblocks = (P.n_groups + 15) / 16;
+        const int lcap = (sblocks + NQ - 1) / NQ * 16;          // most groups of the blocks b = q mod NQ
+        if ((long long)lcap * NQ > s->live_cap) {
+            dfree(s->d_live);
+            HIPCHK(hipMalloc((void**)&s->d_live, (size_t)lcap * NQ * sizeof(int)));
+            s->live_cap = lcap * NQ;
+        }
+        P.gsky = s->d_gsky;
+        P.live = RT_EXP_SKYCMP ? nullptr : s->d_live; P.live_cap = lcap;
+        void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
+        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(1024), sargs, 0, st, e0, nullptr, 0));
+    }
     void* args[] = {&P, &S};
-    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, e0, e1, 0));
+    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
@@ -2570,6 +2703,7 @@ rt_scene::~rt_scene() {
     dfree(d_fnode);
     for (int p = 0; p < 2; p++) { dfree(d_hlist[p]); dfree(d_hflag[p]); }
     dfree(d_hctl);
+    dfree(d_gsky); dfree(d_live);
     dfree(d_tris); dfree(d_meshes); dfree(d_insts); dfree(d_mats); dfree(d_lights); dfree(d_tri_ax);
     dfree(d_node_pair); dfree(d_leaf); dfree(d_inst4); dfree(d_work);
     dfree(d_mesh_box); dfree(d_tree); dfree(d_spp); dfree(d_stats); dfree(d_canvas); dfree(d_dbg);
@@ -2583,7 +2717,7 @@ rt_scene::~rt_scene() {
         Slot& o = store[i];
         dfree(o.d_tree); dfree(o.d_node_pair); dfree(o.d_leaf); dfree(o.d_fnode); dfree(o.d_work);
         for (int p = 0; p < 2; p++) { dfree(o.d_hlist[p]); dfree(o.d_hflag[p]); }
-        dfree(o.d_hctl);
+        dfree(o.d_hctl); dfree(o.d_gsky); dfree(o.d_live);
         dfree(o.d_insts); dfree(o.d_inst4);
         hfree(o.h_insts_pin); hfree(o.h_inst4_pin);
     }
