@@ -209,17 +209,14 @@ struct BvhRefs {
 #ifndef RT_SKY_PREPASS
 #define RT_SKY_PREPASS 1     // sky groups decided and written by sky_kernel before the trace kernel
 #endif
+#ifndef RT_SKY_CONE
+#define RT_SKY_CONE 1        // sky_kernel decides groups by their ray cone first (cone_misses_root)
+#endif
+#ifndef RT_SKY_PERRAY
+#define RT_SKY_PERRAY 1      // sky_kernel runs the exact per-ray test on groups the cone test leaves
+#endif
 #ifndef RT_HIST_GROUPS_PER_WAVE
 #define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
-#endif
-#ifndef RT_EXP_NOTIME
-#define RT_EXP_NOTIME 0      // experiment: no clock reads for the history (every group light)
-#endif
-#ifndef RT_EXP_NOSTORE
-#define RT_EXP_NOSTORE 0     // experiment: flags stored for heavy groups only (stale flags stay)
-#endif
-#ifndef RT_EXP_MEMTIME
-#define RT_EXP_MEMTIME 0     // experiment: history clock = s_memtime (shader clock) instead of the RTC
 #endif
 #ifndef RT_EXP_NOREC
 #define RT_EXP_NOREC 0       // experiment: no duration recording (the history stays the first frame's)
@@ -228,8 +225,12 @@ struct BvhRefs {
 #define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
 #ifndef RT_TPC
-#define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop);
-                             // 3 vs 2: -0.8% world8_stress, -1.3% world8 (profiles/r01/ab_tpc_v33.log)
+#define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop) over all
+                             // groups; 3 vs 2: -0.8% world8_stress, -1.3% world8 (profiles/r01/ab_tpc_v33.log)
+#endif
+#ifndef RT_TPC_LIVE
+#define RT_TPC_LIVE 1        // the same over live-group lists (sky pre-pass): ~8x fewer groups per
+                             // wave, one per ticket balances them (profiles/r02/sky_live_tpc.log)
 #endif
 constexpr int TPC = RT_TPC;
 #ifndef RT_SHADE_LDS
@@ -874,6 +875,7 @@ struct TraceParams {
     // Live-group lists (sky_kernel): queue q's groups are live[q * live_cap + i] for i below
     // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
     const int* live; int live_cap;
+    int tpc;                  // work indices per ticket (normal queues)
 };
 
 // The launch's TraceParams read in place from the kernel-argument segment (constant address
@@ -1297,7 +1299,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         // heavy: over 4x the previous frame's mean group and over 20 us (2000 ticks of the 100 MHz
         // clock) -- in a frame of uniformly cheap groups the mean-relative test alone flags
         // timing noise, and a long heavy list (one atomic per group) is slower than none
-        if (P.hctl_prev[1]) thr = max(4 * P.hctl_prev[1] / (unsigned long long)P.n_groups, (RT_EXP_MEMTIME && !PROF) ? 40000ull : 2000ull);
+        if (P.hctl_prev[1]) thr = max(4 * P.hctl_prev[1] / (unsigned long long)P.n_groups, 2000ull);
     }
     int qi = n_heavy > 0 ? -1 : 0;                           // -1: the previous frame's heavy groups first
     // Lane 0 holds the raw result of the pending ticket request.  A ticket claims TPC
@@ -1308,7 +1310,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     // atomics/s each, which alone bounded a TPC = 1 frame at 0.75 ms (measured, group
     // loop without tracing).
     int pend = 0, inflight = 0;
-    auto step_of = [&](int q) { return q < 0 ? 1 : TPC; };
+    auto step_of = [&](int q) { return q < 0 ? 1 : kparams().tpc; };
     // live lists: tickets [0, 2^k) of a list of n <= 2^k groups visit (t * odd) mod 2^k, a
     // bijection that spreads consecutive tickets over the list (arrival order is roughly
     // raster order, where expensive regions cluster); indices >= n are skipped
@@ -1377,8 +1379,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         if (g >= P.n_groups || (qi < 0 && P.gsky && !RT_EXP_SKYCMP && flag(P.gsky)) ||    // sky group: done by sky_kernel
             (!RT_EXP_NOCHECK && qi >= 0 && P.hist && flag(P.hf_prev)))
             continue;
-        auto hclock = [&]() { return (RT_EXP_MEMTIME && !PROF) ? __builtin_amdgcn_s_memtime() : __builtin_amdgcn_s_memrealtime(); };
-        const unsigned long long g_start = P.hist && !RT_EXP_NOTIME ? hclock() : 0;
+        const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
@@ -1419,7 +1420,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // tree's root -- the traversal's first step, same test -- every sample misses, its
             // radiance is the integrator's initial zero (scene.cu:124-126) and the group's
             // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
-            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && (RT_EXP_SKYCMP || !kparams().gsky) && !__ballot(ft_root_hit(S, bv, act, r0))) {
+            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && (RT_EXP_SKYCMP || !RT_SKY_PERRAY || !kparams().gsky) && !__ballot(ft_root_hit(S, bv, act, r0))) {
                 if (skyflag == 0) skybad = 1;
                 if (act && k == 0) {
                     int op = pix_index;
@@ -1504,7 +1505,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         }
         if (!RT_EXP_NOREC && kparams().hist) {                 // record for the next frame's order
             KTP& P = kparams();
-            const unsigned long long dur = RT_EXP_NOTIME ? 0 : hclock() - g_start;   // wave-uniform (scalar)
+            const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;   // wave-uniform (scalar)
             const bool heavy = dur > thr;
             wave_sum += dur;
             if (lane_id_fresh() == 0) {
@@ -1513,7 +1514,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             int slot = -1;
             if (heavy) slot = atomicAdd(reinterpret_cast<int*>(P.hctl_next), 1);
             const bool rec = heavy && slot < P.heavy_cap;
-            if (!RT_EXP_NOSTORE || rec) P.hf_next[g] = rec ? 1 : 0;
+            P.hf_next[g] = rec ? 1 : 0;
             if (rec) P.hl_next[slot] = g;
             if (P.gdur) {
                 P.gdur[g] = (unsigned)dur;
@@ -1563,54 +1564,155 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
 // each one cost the group loop's whole prologue (ticket, parameter loads, register spills
 // and restores around the integrator) -- a lean, high-occupancy kernel does the test
 // instead.  The root records are read from global memory (all lanes the same address).
-__global__ __launch_bounds__(1024) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
-    __shared__ int s_cnt, s_base;
+// Group-level sky test: the rays of a group leave the camera position through its pixel
+// rectangle [x0, x1] x [y0, y1] (pixels and sample offsets in [0, 1); rows row_step apart
+// are covered by their hull), i.e. they lie in the convex cone spanned by the four corner
+// directions D(cx, cy) = near f + ((cx - W/2) / unit) r + ((H/2 - cy) / unit) u.  A box
+// outside one of the cone's four side half-spaces {x : n . (x - pos) >= 0} meets no ray of
+// the group.  Conservative margins: the rectangle grown by 1/64 pixel (the computed rays'
+// direction rounding is ~1e-6 rad, 1/64 pixel ~1e-5 rad), the box grown by 1e-4 of its
+// coordinate scale, a separation required beyond 1e-5 relative; and the test is only
+// trusted when no direction component comes near zero over the rectangle (|D_a| >= 2^-40
+// |D|), so every ray of the group takes the geometric slab test (no zero-axis skip and
+// no exact-path fallback for tiny components: ray_inv).  A group it does not decide gets
+// the exact per-ray root test.
+__device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const SceneView& S, int g) {
+    const DCamera& c = P.cam;
+    if (!(c.near_ > 0.0f) || S.n_real < 2) return false;
+    const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
+    const int pr0 = gy * P.gh;
+    const float e = 1.0f / 64.0f;
+    const float x0 = (float)(gx * P.gw) - e, x1 = (float)(gx * P.gw + P.gw) + e;
+    const float y0 = (float)(P.row0 + pr0 * P.row_step) - e;
+    const float y1 = (float)(P.row0 + (pr0 + P.gh - 1) * P.row_step + 1) + e;
+    auto D = [&](float cx, float cy) {
+        const float a = (cx - 0.5f * c.W) / c.unit, b = (0.5f * c.H - cy) / c.unit;
+        return (c.near_ * c.f + a * c.r) + b * c.u;
+    };
+    const V3 k0 = D(x0, y0), k1 = D(x1, y0), k2 = D(x1, y1), k3 = D(x0, y1);
+    const V3 mid = D(0.5f * (x0 + x1), 0.5f * (y0 + y1));
+    auto amax = [](V3 v) { return fmaxf(fabsf(v.x), fmaxf(fabsf(v.y), fabsf(v.z))); };
+    const float dmax = fmaxf(fmaxf(amax(k0), amax(k1)), fmaxf(amax(k2), amax(k3)));
+    const float tiny = 0x1p-40f * dmax;
+    auto near0 = [&](float a, float b, float cc, float d) {
+        return fminf(fminf(a, b), fminf(cc, d)) <= tiny && fmaxf(fmaxf(a, b), fmaxf(cc, d)) >= -tiny;
+    };
+    if (near0(k0.x, k1.x, k2.x, k3.x) || near0(k0.y, k1.y, k2.y, k3.y) || near0(k0.z, k1.z, k2.z, k3.z)) return false;
+    V3 n[4] = {cross(k0, k1), cross(k1, k2), cross(k2, k3), cross(k3, k0)};
+#pragma unroll
+    for (int i = 0; i < 4; i++) if (dot(n[i], mid) < 0.0f) n[i] = neg(n[i]);
+    const float4* rec = S.fnode;                               // the root's two children (pair_hit_at)
+    const float4 A = rec[0], B = rec[1], C = rec[2];
+    auto outside = [&](V3 mn, V3 mx, bool nd) {
+        if (!nd) return true;                                  // degenerate: never hit
+        const float m = 1e-4f * (fmaxf(amax(mn), amax(mx)) + amax(c.pos)) + 1e-30f;
+        mn = mn - v3(m, m, m); mx = mx + v3(m, m, m);
+        // a box face plane: the apex beyond it and every direction pointing away from it by
+        // more than the rounding of the computed rays (1e-5 relative)
+        const float away = 1e-5f * dmax;
+        auto face = [&](float o, float lo, float hi, float a0, float a1, float a2, float a3) {
+            return (o > hi && fminf(fminf(a0, a1), fminf(a2, a3)) >= away) || (o < lo && fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) <= -away);
+        };
+        bool sep = face(c.pos.x, mn.x, mx.x, k0.x, k1.x, k2.x, k3.x) || face(c.pos.y, mn.y, mx.y, k0.y, k1.y, k2.y, k3.y) ||
+                   face(c.pos.z, mn.z, mx.z, k0.z, k1.z, k2.z, k3.z);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const V3 q = v3(n[i].x >= 0.0f ? mx.x : mn.x, n[i].y >= 0.0f ? mx.y : mn.y, n[i].z >= 0.0f ? mx.z : mn.z) - c.pos;
+            const float sv = dot(n[i], q);
+            const float tol = 1e-5f * (fabsf(n[i].x) + fabsf(n[i].y) + fabsf(n[i].z)) * (fabsf(q.x) + fabsf(q.y) + fabsf(q.z));
+            sep = sep || sv < -tol;
+        }
+        return sep;
+    };
+    return outside(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), A.x <= B.z) && outside(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), A.y <= B.w);
+}
+
+// One block of 4 waves per 64 consecutive groups: wave 0 runs the cone test, one group per
+// lane; the block writes the outputs of the groups it decided; the 4 waves share the groups it
+// left undecided (exact per-ray test, one group per wave step); the block's live groups are
+// appended to list (block % NQ) with one atomic.  Small blocks keep ~8 per CU resident: the
+// per-ray tests are latency-bound chains (measured: 1024-group blocks, 102 -> 71 us per
+// 1080p frame; per-ray tests of every group, 108 us).
+__global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
+    __shared__ unsigned long long s_sky, s_todo;
+    __shared__ int s_cnt, s_base, s_list[64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, L = P.lanes_per_px;
-    const int g = blockIdx.x * 16 + wv;                        // 16 groups per block, one per wave
-    if (threadIdx.x == 0) s_cnt = 0;
-    bool sky = true;
-    if (g < P.n_groups) {                                      // whole waves
-        const int gy = g / P.n_gx, gx = g - gy * P.n_gx;
-        const int pix_g = lane / L, sub_g = lane - pix_g * L;
-        const int px = gx * P.gw + pix_g % P.gw, pr = gy * P.gh + pix_g / P.gw;
+    const int base = blockIdx.x * 64;
+    const int n_in = min(64, P.n_groups - base);
+    if (wv == 0) {
+        const int gl = base + lane;
+        const bool in = lane < n_in;
+        const bool csky = in && RT_SKY_CONE && cone_misses_root(P, S, gl);
+        const unsigned long long m = __ballot(csky), t = __ballot(in && !csky);
+        if (csky) {
+            gsky[gl] = 1;
+            // the trace kernel records (hf_next) only the groups it runs: a sky group's entry
+            // must not keep a heavy flag from the frame that last wrote this buffer
+            if (P.hist) P.hf_next[gl] = 0;
+        }
+        if (lane == 0) { s_sky = m; s_todo = t; s_cnt = 0; }
+    }
+    __syncthreads();
+    auto sky_pixel = [&](int g, int pix) {                     // pixel pix of sky group g: zeros, -1 hit ids
+        const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
+        const int qx = P.gw_shift >= 0 ? pix & (P.gw - 1) : pix % P.gw;
+        const int qy = P.gw_shift >= 0 ? pix >> P.gw_shift : pix / P.gw;
+        const int px = gx * P.gw + qx, pr = gy * P.gh + qy;
+        if (!(px < P.W && pr < P.n_rows)) return;
+        const int pix_index = P.compact ? pr * P.W + px : (P.row0 + pr * P.row_step) * P.W + px;
+        if (P.hit_inst) P.hit_inst[pix_index] = -1;
+        if (P.hit_tri) P.hit_tri[pix_index] = -1;
+        if (P.rgba) P.rgba[pix_index] = 0u;                   // to_encoding of Color(0, 0, 0, 0)
+        if (P.radiance) P.radiance[pix_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    };
+    const unsigned long long skym = s_sky;
+    if (!RT_EXP_SKYCMP && skym)
+        for (int i = threadIdx.x; i < 64 * P.px_per_wave; i += 256) {
+            const int gi = i / P.px_per_wave;
+            if ((skym >> gi) & 1) sky_pixel(base + gi, i - gi * P.px_per_wave);
+        }
+    // undecided groups: the exact per-ray root test, waves taking every 4th
+    const int pix_g = P.l_shift >= 0 ? lane >> P.l_shift : lane / L;
+    const int sub_g = lane - pix_g * L;
+    const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
+    const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
+    const bool lane_ok = pix_g < P.px_per_wave && sub_g < P.spp;   // k = sub_g (spp <= 64: one round)
+    unsigned long long todo = RT_SKY_PERRAY ? s_todo : 0ull;
+    if (!RT_SKY_PERRAY && threadIdx.x < 64 && ((s_todo >> threadIdx.x) & 1)) {   // undecided: live, the trace kernel tests them
+        gsky[base + threadIdx.x] = 0;
+        s_list[atomicAdd(&s_cnt, 1)] = base + threadIdx.x;
+    }
+    for (int k = 0; todo; k++) {
+        const int bit = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        if ((k & 3) != wv) continue;
+        const int g = base + bit;
+        const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
+        const int px = gx * P.gw + pxo, pr = gy * P.gh + pyo;
         const bool valid = pix_g < P.px_per_wave && px < P.W && pr < P.n_rows;
         const int py = P.row0 + pr * P.row_step;
-        const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;
-        const bool act = valid && sub_g < P.spp;               // k = sub_g (spp <= 64: one round)
+        const bool act = valid && lane_ok;
         Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
         if (act) {
-            const float2 o = spp_offset_dev(sub_g);
+            const float2 o = P.spp_off[sub_g];                 // the host table (same values as spp_offset_dev)
             r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
         }
         BvhRefs bv{};
         bv.fnode = S.fnode;
-        sky = __ballot(ft_root_hit(S, bv, act, r0)) == 0;
+        const bool sky = __ballot(ft_root_hit(S, bv, act, r0)) == 0;
         if (lane == 0) {
             gsky[g] = sky ? 1 : 0;
-            // the trace kernel records (hf_next) only the groups it runs: a sky group's entry
-            // must not keep a heavy flag from the frame that last wrote this buffer
             if (sky && P.hist) P.hf_next[g] = 0;
+            if (!sky) s_list[atomicAdd(&s_cnt, 1)] = g;
         }
-        if (sky && !RT_EXP_SKYCMP) {
-            if (act && sub_g == 0) {
-                if (P.hit_inst) P.hit_inst[pix_index] = -1;
-                if (P.hit_tri) P.hit_tri[pix_index] = -1;
-            }
-            if (valid && sub_g == 0) {
-                if (P.rgba) P.rgba[pix_index] = 0u;           // to_encoding of Color(0, 0, 0, 0)
-                if (P.radiance) P.radiance[pix_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            }
-        }
+        if (sky && !RT_EXP_SKYCMP && valid && sub_g == 0) sky_pixel(g, pix_g);
     }
-    // live groups appended to list (block % NQ): one global atomic per block
     __syncthreads();
-    int slot = 0;
-    if (!sky && lane == 0) slot = atomicAdd(&s_cnt, 1);
+    const int q = blockIdx.x % NQ, n = s_cnt;
+    if (n == 0) return;
+    if (threadIdx.x == 0) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], n);
     __syncthreads();
-    const int q = blockIdx.x % NQ;
-    if (threadIdx.x == 0 && s_cnt > 0) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], s_cnt);
-    __syncthreads();
-    if (!sky && lane == 0) live[q * P.live_cap + s_base + slot] = g;
+    if (threadIdx.x < n) live[q * P.live_cap + s_base + threadIdx.x] = s_list[threadIdx.x];
 }
 
 // Experiment kernel (profiling aid, not on the product path): closest hit of the
@@ -2566,7 +2668,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.scramble_small = (unsigned long long)((P.n_groups + NQ - 1) / NQ + TPC) * (unsigned long long)P.scramble < (1ull << 32);
     P.div_ngx = udiv_make((unsigned)P.n_gx);
     P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
-    P.work = s->d_work;
+    P.work = s->d_work; P.tpc = TPC;
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, WORK_INTS * sizeof(int), st));
     const bool tex = o.textures != 0;
@@ -2660,8 +2762,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
             HIPCHK(hipMalloc((void**)&s->d_gsky, cap));
             s->gsky_cap = cap;
         }
-        const int sblocks = (P.n_groups + 15) / 16;
-        const int lcap = (sblocks + NQ - 1) / NQ * 16;          // most groups of the blocks b = q mod NQ
+        const int sblocks = (P.n_groups + 63) / 64;
+        const int lcap = (sblocks + NQ - 1) / NQ * 64;          // most groups of the blocks b = q mod NQ
         if ((long long)lcap * NQ > s->live_cap) {
             dfree(s->d_live);
             HIPCHK(hipMalloc((void**)&s->d_live, (size_t)lcap * NQ * sizeof(int)));
@@ -2669,8 +2771,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         }
         P.gsky = s->d_gsky;
         P.live = RT_EXP_SKYCMP ? nullptr : s->d_live; P.live_cap = lcap;
+        if (P.live) P.tpc = RT_TPC_LIVE;
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
-        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(1024), sargs, 0, st, e0, nullptr, 0));
+        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(256), sargs, 0, st, e0, nullptr, 0));
     }
     void* args[] = {&P, &S};
     HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));
