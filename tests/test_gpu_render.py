@@ -275,3 +275,48 @@ def test_fast_kernel_exact_spp8_sky_and_horizon(gpu, spp):
         sky_seen |= bool((~hit).all())
         lit_seen |= bool(hit.any() and (~hit).any())
     assert sky_seen and lit_seen
+
+
+def _scene_bounds(s):
+    """World bounds of the scene's triangles (instance translations + mesh vertices; the cube
+    worlds have identity rotations)."""
+    v = s.export("vertices")
+    inst = s.export("instances")
+    lo = inst[:, 4:7].min(0) + v.min(0)                       # instances: quat (4), position (3)
+    hi = inst[:, 4:7].max(0) + v.max(0)
+    return lo, hi
+
+
+@pytest.mark.parametrize("spp,row_step", [(8, 1), (2, 1), (8, 3)])
+def test_sky_prepass_grazing_cones(gpu, spp, row_step):
+    """The sky pre-pass decides most groups by their ray cone (cone_misses_root: side planes
+    and box faces with conservative margins) and writes their outputs itself.  Cameras on and
+    just beside the scene's bounding planes, looking along them, put group cones within
+    rounding of the root boxes: fast frames (pre-pass) == counted frames (no pre-pass) bit
+    for bit, whole frames and row slices."""
+    w, h = 64, 48
+    s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    lo, hi = _scene_bounds(s)
+    mid = 0.5 * (lo + hi)
+    c, sn = np.cos, np.sin
+    quats = [(0.0, 0.0, 0.0, 1.0)]
+    for a in (0.25, 0.5, 0.75, 1.0, 1.5):                      # about y (level views)
+        quats.append((0.0, float(sn(0.5 * np.pi * a)), 0.0, float(c(0.5 * np.pi * a))))
+    for a in (-0.2, 0.2):                                      # tilted up / down
+        quats.append((float(sn(0.5 * np.pi * a)), 0.0, 0.0, float(c(0.5 * np.pi * a))))
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    n = 0
+    for axis in range(3):
+        for side, plane in ((0, lo[axis]), (1, hi[axis])):
+            for off in (0.0, 2e-3, -2e-3, 0.3):
+                pos = mid.copy()
+                pos[axis] = plane + (off if side else -off)
+                for q in quats[:: (1 if axis == 1 else 2)]:
+                    s.set_camera([float(x) for x in pos], q)
+                    kw = dict(spp=spp, want=want, row0=row_step - 1, row_step=row_step, compact=True)
+                    fast = s.render(stats=False, **kw)         # first: the staging buffers hold another pose
+                    full = s.render(stats=True, **kw)
+                    for k in want:
+                        assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (axis, side, off, q, k)
+                    n += 1
+    assert n > 60

@@ -1,4 +1,5 @@
-"""Turn a tools/profile.sh run into profiles/pmc_traffic.json (HBM bytes per trace launch)
+"""Turn a tools/profile.sh run into profiles/pmc_traffic.json (HBM bytes per trace stage:
+the trace kernel plus the sky pre-pass of fast frames)
 and a short markdown summary.
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3's derived memory-side (TCC EA) counters in KiB.
@@ -25,6 +26,19 @@ def is_timed_trace(name):
     return mode.isdigit() and (int(mode) & 2) == 0          # MODE bit 1 = STATS
 
 
+def is_sky(name):
+    """The sky pre-pass of the fast frames: part of the trace stage."""
+    return "sky_kernel" in name
+
+
+def stage(root, counter):
+    """Per frame of the trace stage: the trace kernel's mean per dispatch plus the sky
+    pre-pass's (when the profile has one)."""
+    a, n = per_dispatch(root, counter)
+    b, _ = per_dispatch(root, counter, is_sky)
+    return (None, 0) if a is None else (a + (b or 0.0), n)
+
+
 def per_dispatch(root, counter, sel=is_timed_trace):
     vals = collections.defaultdict(float)
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
@@ -47,12 +61,13 @@ def kernel_stats(root, sel=is_timed_trace):
 def main():
     root, key, W, rows = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
     out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
-    fetch_kib, nf = per_dispatch(root, "FETCH_SIZE")
-    write_kib, nw = per_dispatch(root, "WRITE_SIZE")
-    rdreq, _ = per_dispatch(root, "TCC_EA0_RDREQ_sum")
-    wrreq, _ = per_dispatch(root, "TCC_EA0_WRREQ_sum")
-    issue = {c: per_dispatch(root, c)[0] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
-                                                  "SQ_WAIT_ANY")}
+    fetch_kib, nf = stage(root, "FETCH_SIZE")
+    write_kib, nw = stage(root, "WRITE_SIZE")
+    rdreq, _ = stage(root, "TCC_EA0_RDREQ_sum")
+    wrreq, _ = stage(root, "TCC_EA0_WRREQ_sum")
+    issue = {c: stage(root, c)[0] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                                           "SQ_WAIT_ANY")}
+    issue_sky = {c: per_dispatch(root, c, is_sky)[0] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU")}
     if fetch_kib is None or write_kib is None:
         sys.exit("no FETCH_SIZE/WRITE_SIZE rows for trace_kernel under " + root)
     frame_bytes = 4 * W * rows
@@ -65,8 +80,12 @@ def main():
                 "TCC_EA0_RDREQ": rdreq, "TCC_EA0_WRREQ": wrreq},
         "write_calibration": {"frame_store_bytes": frame_bytes, "write_over_frame": wr / frame_bytes},
         "kernel_trace": kernel_stats(root),
+        "kernel_trace_sky": kernel_stats(root, is_sky),
+        # per frame: trace kernel + sky pre-pass (the trace stage bench.py's events span)
+        "stage": "sky_kernel + trace_kernel",
         # wave-level instruction counts per launch (secondary bound: VALU issue, bench.py)
         "issue": {k: v for k, v in issue.items() if v is not None},
+        "issue_sky_kernel": {k: v for k, v in issue_sky.items() if v is not None},
         "source": os.path.relpath(root),
     }
     db = json.load(open(out)) if os.path.exists(out) else {}
