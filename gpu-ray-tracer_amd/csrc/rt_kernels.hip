@@ -212,6 +212,9 @@ struct BvhRefs {
 #ifndef RT_SKY_CONE
 #define RT_SKY_CONE 1        // sky_kernel decides groups by their ray cone first (cone_misses_root)
 #endif
+#ifndef RT_UNLIT_SKIP
+#define RT_UNLIT_SKIP 1      // fast frames skip shadow rays of lights with a zero phong factor
+#endif
 #ifndef RT_SKY_PERRAY
 #define RT_SKY_PERRAY 1      // sky_kernel runs the exact per-ray test on groups the cone test leaves
 #endif
@@ -813,16 +816,20 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
 // Shading: phong.cu:14-53, light.cu:11-77, scene.cu:14-22
 // ---------------------------------------------------------------------------
 // kd: the material's Kd (the reference), or the atlas texel in the textured mode
-__device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
-#if RT_EXP_NOPHONG                                             // experiment: shading arithmetic priced (wrong colours)
-    return incoming + kd;
-#endif
+// diffuse + specular: phong's factor of the incoming light
+__device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_dir, V3 to_light) {
     float nd = max_std(dot(to_light, nrm), 0.0f);
     V4 diffuse = nd * kd;
     V3 reflected = reflect(neg(to_light), nrm);
     float rd = dot(neg(reflected), ray_dir);
     V4 specular = pow_fast(max_std(rd, 0.0f), m.alpha) * m.Ks;
-    return (diffuse + specular) * incoming;
+    return diffuse + specular;
+}
+__device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
+#if RT_EXP_NOPHONG                                             // experiment: shading arithmetic priced (wrong colours)
+    return incoming + kd;
+#endif
+    return phong_factor(m, kd, nrm, ray_dir, to_light) * incoming;
 }
 
 // RayFrame (scene.cu:81-90).  The top frame's hit point and normal are not kept in
@@ -876,6 +883,7 @@ struct TraceParams {
     // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
     const int* live; int live_cap;
     int tpc;                  // work indices per ticket (normal queues)
+    int unlit_skip;           // fast frames: no shadow segments for a light whose phong factor is zero
 };
 
 // The launch's TraceParams read in place from the kernel-argument segment (constant address
@@ -1033,6 +1041,20 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                         max_t = INFINITY;
                     }
                     rv = L.col;                                    // Light::attenuate (light.cu:30-31)
+                    // Unlit skip: when phong's factor (diffuse + specular) is zero in every
+                    // channel -- the light behind the surface, no specular lobe -- the light's
+                    // term (factor x incoming) is that signed zero for every incoming light
+                    // >= +0, which the host guarantees (unlit_skip: light colours >= +0 and
+                    // finite, transmission Kt in [+0, 1], so every attenuation is >= +0 and
+                    // finite).  The shadow segments cannot change the sum: none is traced.
+                    // The lane still takes the wait-for-shadow step, with no query (max_t = -inf
+                    // marks it): no hit, so the light's term is phong's with the unshadowed
+                    // light, the same signed zeros.
+                    if (P.unlit_skip) {
+                        const DMat& mm = bv.mats[is_mat];
+                        const V4 f = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl);
+                        if (f.x == 0.0f && f.y == 0.0f && f.z == 0.0f && f.w == 0.0f) max_t = -INFINITY;
+                    }
                     q = make_ray(at(to, THRESH), to.d);
                     dbg(P, me, 4);
                     st = ST_WAIT_SHADOW;
@@ -1104,7 +1126,9 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
-        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(S, bv, need, q, b, wc, occl, lim);
+        // (an unlit-skipped shadow step, max_t = -inf, takes no query)
+        const bool qa = st == ST_WAIT_NORMAL || (st == ST_WAIT_SHADOW && max_t >= 0.0f);
+        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(S, bv, qa, q, b, wc, occl, lim);
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -2669,6 +2693,15 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.div_ngx = udiv_make((unsigned)P.n_gx);
     P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
     P.work = s->d_work; P.tpc = TPC;
+    {   // unlit skip (trace_sample, ST_LIGHT): every incoming light must be >= +0 and finite
+        bool ok = RT_UNLIT_SKIP && !want_stats && !dbg && !prof;
+        auto pos0 = [](float v) { return std::isfinite(v) && !std::signbit(v); };
+        for (const DLight& l : h.d_lights) ok = ok && pos0(l.col.x) && pos0(l.col.y) && pos0(l.col.z) && pos0(l.col.w);
+        for (const DMat& m : h.d_mats)
+            ok = ok && pos0(m.Kt.x) && pos0(m.Kt.y) && pos0(m.Kt.z) && pos0(m.Kt.w) && m.Kt.x <= 1.0f && m.Kt.y <= 1.0f &&
+                 m.Kt.z <= 1.0f && m.Kt.w <= 1.0f;
+        P.unlit_skip = ok ? 1 : 0;
+    }
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, WORK_INTS * sizeof(int), st));
     const bool tex = o.textures != 0;

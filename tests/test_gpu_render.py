@@ -320,3 +320,46 @@ def test_sky_prepass_grazing_cones(gpu, spp, row_step):
                         assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (axis, side, off, q, k)
                     n += 1
     assert n > 60
+
+
+@pytest.mark.parametrize("col1", [(0.9, 0.8, 0.7, 1.0), (0.9, -0.0, 0.7, 1.0)])
+def test_unlit_skip_exact(gpu, col1):
+    """The fast kernels trace no shadow segments for a light whose phong factor (diffuse +
+    specular) is zero in every channel; the light's term is then that signed zero whatever the
+    shadow, so frames equal the counted kernel's (every shadow ray traced) bit for bit.  A
+    built scene with opaque, specular (small and large alpha), refractive (Kt in (0, 1)) and
+    reflective cubes, lights from above and below (back-facing for many faces) and cameras
+    all around.  A light colour with a -0 channel makes the skip unsound (-0 x 0 vs +0 x 0)
+    and the host turns it off: the frames must still agree."""
+    m = gpu.material
+    mats = [m(Ka=(0.1, 0.1, 0.1, 1), Kd=(0.6, 0.3, 0.1, 1)),
+            m(Ka=(0.1, 0.1, 0.1, 1), Kd=(0.2, 0.5, 0.2, 1), Ks=(0.8, 0.8, 0.8, 1), alpha=0.3),
+            m(Kd=(0.2, 0.2, 0.6, 1), Kt=(0.5, 0.6, 0.7, 1), eta=1.3),
+            m(Kd=(0.3, 0.3, 0.3, 1), Ks=(0.5, 0.5, 0.5, 1), Kr=(0.7, 0.7, 0.7, 1), alpha=8.0)]
+    s = gpu.Scene.create()
+    meshes = [s.build_cube(1.0, mt) for mt in mats]
+    rng = np.random.default_rng(5)
+    for i in range(5):
+        for j in range(5):
+            t = s.add_trans(meshes[(i + 2 * j) % 4])
+            s.set_trans(t, pos=(1.6 * i - 3.2, float(rng.integers(0, 3)), 1.6 * j - 3.2))
+    s.add_point_light((0.5, 6.0, 0.3), (1.0, 1.0, 1.0, 1.0))
+    s.add_directional_light((0.3, -1.0, 0.8), col1)
+    s.add_directional_light((-0.2, 1.0, -0.4), (0.4, 0.5, 0.6, 1.0))   # from below
+    s.finish(96, 64, 60.0, 100.0, cam_pos=(0.0, 9.0, -9.0), cam_quat=(-0.3826834, 0.0, 0.0, 0.9238795),
+             dist_atten=(0.1, 0.05, 0.01), ambience=(0.2, 0.2, 0.2, 1.0), depth=3)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    poses = [((0.0, 9.0, -9.0), (-0.3826834, 0.0, 0.0, 0.9238795))]
+    for _ in range(6):
+        q = rng.normal(size=4)
+        poses.append(((float(rng.uniform(-6, 6)), float(rng.uniform(-2, 8)), float(rng.uniform(-6, 6))),
+                      tuple(float(x) for x in q / np.linalg.norm(q))))
+    lit = 0.0
+    for pos, q in poses:
+        s.set_camera(pos, q)
+        fast = s.render(spp=4, want=want, stats=False)
+        full = s.render(spp=4, want=want, stats=True)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, q, k)
+        lit += (full["hit_inst"] >= 0).mean()
+    assert lit / len(poses) > 0.05
