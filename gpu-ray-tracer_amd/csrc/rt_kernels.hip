@@ -243,6 +243,9 @@ constexpr int TPC = RT_TPC;
 #define RT_ZERO_AXIS_CUT 1   // 0: A/B variant, zero-direction axes unconstrained as in the reference (closest_hit)
 #endif
 constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
+#ifndef RT_TRAV2
+#define RT_TRAV2 1           // compact fast-traversal step (closest_hit); 0: the previous step, A/B
+#endif
 #ifndef RT_PK_PAIR
 #define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
                              //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
@@ -359,6 +362,39 @@ __device__ __forceinline__ void pair_hit_tt(const float4* rec, const Ray& r, con
     if (__builtin_expect(__ballot(x0 || x1) != 0, 0)) {
         if (x0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
         if (x1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
+    }
+}
+// pair_hit_tt for the compact traversal step (RT_TRAV2).  Every record of the ordered tree is a
+// proper finite box (the host leaves a frame with a degenerate or non-finite real box to the heap
+// kernels: ordered_tree_shape), so there is no per-child degenerate test; a ray that needs the
+// exact test everywhere (ri.exact) enters with NaN reciprocals (closest_hit), so both its slab
+// results are NaN and both outcome tests are false: it takes the exact test with no filtered-ray
+// mask.  ta/tb carry no activity mask: an inactive lane's cut is NaN, so t <= cut is false for it.
+__device__ __forceinline__ void pair_hit_tt2(const float4* rec, const Ray& r, const RayInv& ri, bool active,
+                                             float& ta, float& tb) {
+    const float4 A = rec[0], B = rec[1], C = rec[2];
+    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
+        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
+        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
+        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
+        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
+        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
+    };
+    float lo0, hi0, lo1, hi1;
+    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
+    const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS);
+    const float el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
+    const float d0 = lo0 - el0, d1 = lo1 - el1;
+    const bool hc0 = fmaxf(lo0 + el0, THRESH) <= hi0 - eh0, hc1 = fmaxf(lo1 + el1, THRESH) <= hi1 - eh1;
+    const bool mc0 = fmaxf(d0, THRESH) > hi0 + eh0, mc1 = fmaxf(d1, THRESH) > hi1 + eh1;
+    const float QNAN = __builtin_nanf("");
+    ta = hc0 ? d0 : QNAN;
+    tb = hc1 ? d1 : QNAN;
+    const bool k0 = hc0 || mc0, k1 = hc1 || mc1;               // outcome certain
+    if (__builtin_expect(__ballot(active && !(k0 && k1)) != 0, 0)) {
+        if (active && !k0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
+        if (active && !k1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
     }
 }
 __device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
@@ -672,6 +708,75 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // leaf improves the closest hit: recomputed after each leaf visit, not every step.
         const float QNAN = __builtin_nanf("");
         float ct = !active_in ? QNAN : prune ? cut() : INFINITY;
+#if RT_TRAV2
+        // Compact step (same visits, same order), one loop latch: a step either descends into
+        // A (B pushed when hit) or runs up to two leaves at the single leaf site (A then B) and
+        // continues at an internal B or pops.  A popped "leaf B of node X" re-runs X's pair test
+        // and goes straight to the leaf site.  A leaf A before an internal B no longer pushes B
+        // (the stack holds no more than before).  Pushes are v_writelane into the stack VGPR.
+        // Same-box A/B (profiles/r02/ab_trav2.log): frame 0.833 -> 0.810 ms, trace 0.973 -> 0.952.
+        if (ri.exact) ri.ix = ri.iy = ri.iz = QNAN;           // every box: the exact test (pair_hit_tt2)
+        int node = 0, sp = 0, stk = 0, bonly = 0;
+        auto push = [&](int e) { asm("v_writelane_b32 %0, %1, m0" : "+v"(stk) : "s"(e), "{m0}"(sp)); sp++; };
+        for (;;) {
+            const float4* rec = bv.fnode + 4 * node;
+            if (PROF) wc.wpair++;
+            exp_pad<1>();                                      // experiment: per child-pair step
+            const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
+            const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
+            float ta, tb;
+            pair_hit_tt2(rec, r, ri, ct == ct, ta, tb);
+            float lt = QNAN, t2 = QNAN;                        // leaf entry bounds (NaN: missed)
+            int linst = -1, inst2 = -1, next = -1;             // their instances, the next node (uniform; -1: pop)
+            if (bonly) {                                       // popped: leaf B of this node
+                bonly = 0;
+                lt = tb; linst = -1 - rb;
+            } else {
+                const bool hA = __ballot(ta <= ct) != 0, hB = __ballot(tb <= ct) != 0;
+                if (ra >= 0 && hA) {                           // descend into A, B after A's subtree
+                    next = ra;
+                    if (hB) push(rb >= 0 ? rb : -2 - node);
+                } else {
+                    if (hA) { lt = ta; linst = -1 - ra; }      // leaf A (ra < 0 here)
+                    if (hB) {
+                        if (rb >= 0) next = rb;                // after leaf A, if any
+                        else if (linst >= 0) { t2 = tb; inst2 = -1 - rb; }
+                        else { lt = tb; linst = -1 - rb; }
+                    }
+                }
+            }
+            if (linst >= 0) {
+                for (;;) {                                     // the leaf site: one or two leaves
+                    const bool lh = lt <= ct;                  // (ct only decreases: fresh for the second leaf)
+                    if (__ballot(lh)) {
+                        exp_pad<2>();                          // experiment: per leaf visit
+                        if (!pre_ok) {
+                            if (AXIS) pre = dir_pre<true>(r.d);    // S.tri_ax set: identity rotations
+                            else if (S.ident_all) pre = dir_pre(r.d);
+                            pre_ok = true;
+                        }
+                        const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+                        if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
+                        if (lh && cast_local<false, AXIS, PROF>(S, bv, linst, r, b, pre, wc, t_low(lt)))
+                            if (b.time <= occl_t) ct = QNAN;   // occluded: this lane is done
+                        if (prune && ct == ct) ct = cut();
+                        if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
+                        if (!__ballot(ct == ct)) { next = -2; break; }   // every lane occluded
+                    }
+                    if (inst2 < 0) break;
+                    lt = t2; linst = inst2; inst2 = -1;
+                }
+                if (next == -2) break;
+            }
+            if (next >= 0) { node = next; continue; }
+            if (sp == 0) break;
+            sp--;                                              // an internal node, or leaf B of node -2 - e
+            const int e = __builtin_amdgcn_readlane(stk, sp);
+            if (e < 0) { node = -2 - e; bonly = 1; }
+            else node = e;
+        }
+        return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
+#else
         int node = 0, sp = 0, stk = 0, bonly = 0, has2 = 0, inst2 = 0;
         float t2 = QNAN;
         const int my_lane = __lane_id();
@@ -740,6 +845,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             else node = e;
         }
         return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
+#endif
     }
     if (STATS) wc.nodes += __popcll(am);                       // root test
     bool hr, hdummy;
@@ -2338,14 +2444,24 @@ std::vector<Box> mesh_boxes(const rt::Scene& h) {
 void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
     const std::vector<Box> mbox = mesh_boxes(h);
     std::vector<std::pair<unsigned long long, int>> kv;
+    bool ordered = true;                                      // every real box finite with mn <= mx
     for (size_t i = 0; i < h.d_insts.size(); i++) {
         const Box b = from_local(mbox[h.d_insts[i].mesh], h.d_insts[i].pose);
-        if (b.nd) kv.push_back({z_order(neg(box_center(b))), (int)i});
+        if (b.nd) {
+            kv.push_back({z_order(neg(box_center(b))), (int)i});
+            const float c[6] = {b.mn.x, b.mn.y, b.mn.z, b.mx.x, b.mx.y, b.mx.z};
+            for (float x : c) ordered = ordered && std::isfinite(x);
+            ordered = ordered && b.mn.x <= b.mx.x && b.mn.y <= b.mx.y && b.mn.z <= b.mx.z;
+        }
     }
     std::stable_sort(kv.begin(), kv.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
     const int nr = (int)kv.size();
     *n_real = nr;
     *depth = 0;
+    // The fast traversal takes every record of the ordered tree as a proper box (no
+    // degenerate / NaN test per child, pair_hit_tt): a pose that makes a box non-finite
+    // leaves the frame to the heap kernels.
+    if (!ordered) { *depth = 1 << 20; return; }
     if (nr < 2) return;
     std::vector<unsigned long long> keys(nr);
     for (int i = 0; i < nr; i++) keys[i] = kv[i].first;
