@@ -198,6 +198,27 @@ def test_fast_kernel_exact_zero_direction_axes(gpu):
             assert (full["hit_inst"] >= 0).mean() > 0.05, pos          # (a centre row may run in a gap)
 
 
+def test_fast_kernel_exact_tiny_direction_components(gpu):
+    """Rays outside the filtered slab test's range (0 < |d_a| < 2^-64: ray_inv's exact flag),
+    which the fast traversal sends to the exact reference test at every node (NaN
+    reciprocals, pair_hit_tt2): level cameras turned by 1e-25..1e-21 rad, so the centre
+    column's / row's sample-0 rays carry such a component, among ordinary rays."""
+    import math
+    s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    e = 0.4995
+    for pos in ([e, 3 + e, -8.0], [-2 - e, 6 - e, -7.5], [0.3, 4.2, -6.0]):
+        for ax, ang in ((1, 1e-25), (0, -3e-22), (1, -7e-21), (2, 1e-23)):
+            q = [0.0, 0.0, 0.0, math.cos(ang / 2)]
+            q[ax] = math.sin(ang / 2)
+            s.set_camera(pos, q)
+            fast = s.render(spp=2, want=want, stats=False)
+            full = s.render(spp=2, want=want, stats=True)
+            for k in want:
+                assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, ax, ang, k)
+            assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+
+
 def test_fast_kernel_exact_random_cameras(gpu):
     """Fast kernel (ordered LBVH, pruning, axis-plane triangle path with its shared-plane
     skip and in-plane reject) == counted reference-heap kernel, bit for bit, from seeded
