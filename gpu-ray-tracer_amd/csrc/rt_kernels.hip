@@ -246,6 +246,10 @@ constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
 #ifndef RT_TRAV2
 #define RT_TRAV2 1           // compact fast-traversal step (closest_hit); 0: the previous step, A/B
 #endif
+#ifndef RT_ANYASM
+#define RT_ANYASM 2          // 1: the step's two wave hits as 0/1 SGPR integers (any_lane); 2: also the
+                             // exact-fallback test (same-box A/B, profiles/r02/ab_anyasm.log: 0.806 -> 0.797 ms)
+#endif
 #ifndef RT_PK_PAIR
 #define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
                              //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
@@ -364,6 +368,13 @@ __device__ __forceinline__ void pair_hit_tt(const float4* rec, const Ray& r, con
         if (x1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
     }
 }
+// 0/1 in an SGPR from a wave mask, opaque to the optimizer (a boolean taken from a ballot is
+// otherwise rebuilt through a VGPR: v_cndmask + v_cmp per use)
+__device__ __forceinline__ unsigned any_lane(unsigned long long m) {
+    unsigned h;
+    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(h) : "s"(m) : "scc");
+    return h;
+}
 // pair_hit_tt for the compact traversal step (RT_TRAV2).  Every record of the ordered tree is a
 // proper finite box (the host leaves a frame with a degenerate or non-finite real box to the heap
 // kernels: ordered_tree_shape), so there is no per-child degenerate test; a ray that needs the
@@ -392,7 +403,11 @@ __device__ __forceinline__ void pair_hit_tt2(const float4* rec, const Ray& r, co
     ta = hc0 ? d0 : QNAN;
     tb = hc1 ? d1 : QNAN;
     const bool k0 = hc0 || mc0, k1 = hc1 || mc1;               // outcome certain
+#if RT_ANYASM >= 2
+    if (__builtin_expect(any_lane(__ballot(active && !(k0 && k1))), 0)) {
+#else
     if (__builtin_expect(__ballot(active && !(k0 && k1)) != 0, 0)) {
+#endif
         if (active && !k0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
         if (active && !k1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
     }
@@ -732,7 +747,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 bonly = 0;
                 lt = tb; linst = -1 - rb;
             } else {
+#if RT_ANYASM
+                const unsigned hA = any_lane(__ballot(ta <= ct)), hB = any_lane(__ballot(tb <= ct));
+#else
                 const bool hA = __ballot(ta <= ct) != 0, hB = __ballot(tb <= ct) != 0;
+#endif
                 if (ra >= 0 && hA) {                           // descend into A, B after A's subtree
                     next = ra;
                     if (hB) push(rb >= 0 ? rb : -2 - node);
@@ -761,12 +780,11 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                             if (b.time <= occl_t) ct = QNAN;   // occluded: this lane is done
                         if (prune && ct == ct) ct = cut();
                         if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
-                        if (!__ballot(ct == ct)) { next = -2; break; }   // every lane occluded
+                        if (!__ballot(ct == ct)) { next = -1; sp = 0; break; }   // every lane occluded: done
                     }
                     if (inst2 < 0) break;
                     lt = t2; linst = inst2; inst2 = -1;
                 }
-                if (next == -2) break;
             }
             if (next >= 0) { node = next; continue; }
             if (sp == 0) break;
