@@ -118,6 +118,7 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const float4* node_pair;  // BVH child pairs, heap order (written by bvh_build_kernel), see BvhRefs
     const float4* fnode;      // ordered LBVH of the fast kernel (bvh_build_kernel)
     int n_real, ftree;        // its leaf count; 1 if usable (>= 2 leaves, depth <= 31)
+    int n_quad;               // RT_QUAD: its 4-wide records (binary nodes at even depth), after the binary ones
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
@@ -243,6 +244,11 @@ constexpr int TPC = RT_TPC;
 #define RT_ZERO_AXIS_CUT 1   // 0: A/B variant, zero-direction axes unconstrained as in the reference (closest_hit)
 #endif
 constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
+#ifndef RT_QUAD
+#define RT_QUAD 0            // 1: A/B variant, fast traversal over 4-wide records (bvh_build_kernel's quad
+                             // phase): bit-exact (69 GPU tests) but +5% frame (profiles/r02/ab_quad.log)
+#endif
+constexpr int QEMPTY = (int)0x80000000;   // empty slot of a quad record
 #ifndef RT_TRAV2
 #define RT_TRAV2 1           // compact fast-traversal step (closest_hit); 0: the previous step, A/B
 #endif
@@ -625,7 +631,7 @@ __device__ __forceinline__ bool ft_root_hit(const SceneView& S, const BvhRefs& b
     zero_axis_cut(S, r, ri);
     bool h0, h1;
     float t0, t1;
-    pair_hit_at(bv.fnode, r, ri, active, h0, h1, t0, t1);
+    pair_hit_at(RT_QUAD ? S.fnode : bv.fnode, r, ri, active, h0, h1, t0, t1);   // the binary root record
     return h0 || h1;
 }
 
@@ -733,6 +739,87 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         if (ri.exact) ri.ix = ri.iy = ri.iz = QNAN;           // every box: the exact test (pair_hit_tt2)
         int node = 0, sp = 0, stk = 0, bonly = 0;
         auto push = [&](int e) { asm("v_writelane_b32 %0, %1, m0" : "+v"(stk) : "s"(e), "{m0}"(sp)); sp++; };
+#if RT_QUAD
+        // 4-wide step (bvh_build_kernel's quad records): the four slots (A's children or A, then
+        // B's) are tested in one LDS round trip; hit leaves before the first hit internal slot run
+        // now, in slot order, at the single leaf site; the first hit internal slot is the next
+        // node; hit slots after it are pushed in reverse order (a leaf as -2 - (4 node + slot),
+        // re-tested when popped: bonly = slot + 1).  Same leaves, same order as the binary walk.
+        // The stack holds <= 3 entries per quad level: <= 48 for binary depth <= 31 (host check).
+        (void)bonly;
+        int pslot = -1;                                        // popped leaf entry: its slot
+        // guards against malformed records (never taken on a tree the build kernel wrote): every
+        // wave leaves the loop within 2^16 steps, leaf ids outside the instance range are skipped
+        for (int guard = 0; guard < (1 << 16); guard++) {
+            const float4* rec = bv.fnode + 7 * node;
+            if (PROF) wc.wpair++;
+            exp_pad<1>();                                      // experiment: per step
+            const int4 rf = *reinterpret_cast<const int4*>(rec + 6);
+            const int r0 = uni(rf.x), r1 = uni(rf.y), r2 = uni(rf.z), r3 = uni(rf.w);
+            float t0, t1, t2, t3;
+            unsigned lv, nxt_bit = 0;                          // slots to run at the leaf site now
+            int next = -1;
+            if (pslot >= 0) {                                  // popped leaf: its pair only
+                const int ps = pslot;
+                pslot = -1;
+                float ta, tb;
+                pair_hit_tt2(rec + 3 * (ps >> 1), r, ri, ct == ct, ta, tb);
+                t0 = t1 = t2 = t3 = (ps & 1) ? tb : ta;        // (only slot ps is read)
+                lv = 1u << ps;
+            } else {
+                pair_hit_tt2(rec, r, ri, ct == ct, t0, t1);
+                pair_hit_tt2(rec + 3, r, ri, ct == ct, t2, t3);
+                const unsigned h = (any_lane(__ballot(t0 <= ct)) & (unsigned)(r0 != QEMPTY)) |
+                                   ((any_lane(__ballot(t1 <= ct)) & (unsigned)(r1 != QEMPTY)) << 1) |
+                                   ((any_lane(__ballot(t2 <= ct)) & (unsigned)(r2 != QEMPTY)) << 2) |
+                                   ((any_lane(__ballot(t3 <= ct)) & (unsigned)(r3 != QEMPTY)) << 3);
+                const unsigned im = (unsigned)(r0 >= 0) | ((unsigned)(r1 >= 0) << 1) | ((unsigned)(r2 >= 0) << 2) |
+                                    ((unsigned)(r3 >= 0) << 3);
+                const unsigned hi = h & im;
+                const int f = hi ? __builtin_ctz(hi) : 4;      // first hit internal slot
+                lv = h & ((1u << f) - 1u);                     // hit leaves before it
+                if (f < 4) {
+                    next = f == 0 ? r0 : f == 1 ? r1 : f == 2 ? r2 : r3;
+                    nxt_bit = h & ~((2u << f) - 1u);           // hit slots after it
+                    for (int i = 3; i > f; i--)
+                        if ((nxt_bit >> i) & 1u) {
+                            const int ri_ = i == 1 ? r1 : i == 2 ? r2 : r3;
+                            push(ri_ >= 0 ? ri_ : -2 - (4 * node + i));
+                        }
+                }
+            }
+            while (lv) {                                       // the leaf site, slots in order
+                const int sl = __builtin_ctz(lv);
+                lv &= lv - 1u;
+                const float lt = sl == 0 ? t0 : sl == 1 ? t1 : sl == 2 ? t2 : t3;
+                const int linst = -1 - (sl == 0 ? r0 : sl == 1 ? r1 : sl == 2 ? r2 : r3);
+                if ((unsigned)linst >= (unsigned)S.n_inst) continue;
+                const bool lh = lt <= ct;                      // (ct only decreases)
+                if (__ballot(lh)) {
+                    exp_pad<2>();                              // experiment: per leaf visit
+                    if (!pre_ok) {
+                        if (AXIS) pre = dir_pre<true>(r.d);    // S.tri_ax set: identity rotations
+                        else if (S.ident_all) pre = dir_pre(r.d);
+                        pre_ok = true;
+                    }
+                    const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
+                    if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
+                    if (lh && cast_local<false, AXIS, PROF>(S, bv, linst, r, b, pre, wc, t_low(lt)))
+                        if (b.time <= occl_t) ct = QNAN;       // occluded: this lane is done
+                    if (prune && ct == ct) ct = cut();
+                    if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
+                    if (!__ballot(ct == ct)) { next = -1; sp = 0; break; }   // every lane occluded: done
+                }
+            }
+            if (next >= 0) { node = next; continue; }
+            if (sp == 0) break;
+            sp--;                                              // a quad node, or leaf slot s of node n: -2 - (4 n + s)
+            const int e = __builtin_amdgcn_readlane(stk, sp);
+            if (e < 0) { node = (-2 - e) >> 2; pslot = (-2 - e) & 3; }
+            else node = e;
+        }
+        return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
+#endif
         for (;;) {
             const float4* rec = bv.fnode + 4 * node;
             if (PROF) wc.wpair++;
@@ -1347,7 +1434,7 @@ __host__ __device__ inline size_t shade_bytes(const SceneView& S) {
 }
 __host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false) {
     const size_t sh = shade ? shade_bytes(S) : 0;
-    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
+    if (ft) return (RT_QUAD ? 112 * (size_t)S.n_quad : 64 * (size_t)(S.n_real - 1)) + 16 * (size_t)S.n_inst + sh;
     return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
 }
 // word copy of n records of T into LDS at `dst` (block-cooperative)
@@ -1365,7 +1452,8 @@ template <class T> __device__ __forceinline__ const T* stage_words(unsigned char
 template <bool LDS, bool FT = false, bool SHADE = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
-    bv.fnode = S.fnode; bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
+    bv.fnode = RT_QUAD ? S.fnode + 4 * (S.n_real - 1) : S.fnode;   // the traversal's records (quad: after the binary ones)
+    bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
     bv.mats = S.mats; bv.lights = S.lights; bv.tris = S.tris; bv.meshes = S.meshes;
     if (LDS && SHADE) {                                    // after the BVH image (lds_bytes without the cache)
         unsigned char* p = smem + lds_bytes(S, FT);
@@ -1375,10 +1463,11 @@ __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* 
         bv.meshes = stage_words(p, S.meshes, S.n_meshes);
     }
     if (LDS && FT) {                                       // ordered LBVH | inst4
-        const int nf = 4 * (S.n_real - 1);
+        const int nf = RT_QUAD ? 7 * S.n_quad : 4 * (S.n_real - 1);             // quad records only
+        const float4* src = RT_QUAD ? S.fnode + 4 * (S.n_real - 1) : S.fnode;
         float4* fn = reinterpret_cast<float4*>(smem);
         float4* in = fn + nf;
-        for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = S.fnode[i];
+        for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = src[i];
         for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
         __syncthreads();
         bv.fnode = fn; bv.inst = in;
@@ -2163,6 +2252,66 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         refs[2] = refs[3] = 0;
     }
     BSTAMP(6);
+#if RT_QUAD
+    // 4-wide records of the fast kernel (QNode, after the binary records): binary node i at
+    // even depth (the root at 0) becomes quad node qid[i], whose four slots are its children's
+    // children in DFS order -- child A's two children (or A itself when A is a leaf, then an
+    // empty slot), then B's.  The internal slots are binary nodes at even depth again.  The set
+    // of leaves a ray hits and their order are those of the binary tree (a hit leaf's ancestors
+    // are hit: the slab test is monotone in the box), the skipped odd-depth boxes only cull.
+    // Layout per quad node: 7 float4 = pair (slot 0, 1) and pair (slot 2, 3) in the binary
+    // record's interleaved form, then the four refs (node index >= 0, -1 - instance for a leaf,
+    // QEMPTY).  The LDS of the phases above is reused: par | qid | 16 wave partials.
+    __syncthreads();
+    if (nr >= 2) {
+        const int m = nr - 1;                                  // binary internal nodes
+        int* par = reinterpret_cast<int*>(smem);
+        int* qid = par + m;
+        int* wsum = qid + m;
+        auto bref = [&](int i, int c) { return reinterpret_cast<const int*>(A.fnode + 4 * (size_t)i + 3)[c]; };
+        for (int i = tid; i < m; i += nt) par[i] = -1;
+        __syncthreads();
+        for (int i = tid; i < m; i += nt)
+            for (int c = 0; c < 2; c++) { const int ch = bref(i, c); if (ch >= 0) par[ch] = i; }
+        __syncthreads();
+        const int chunk = (m + nt - 1) / nt, b0 = min(m, tid * chunk), b1 = min(m, b0 + chunk);
+        int cnt = 0;
+        for (int i = b0; i < b1; i++) {
+            int d = 0;
+            for (int p = par[i]; p >= 0 && d < 64; p = par[p]) d++;
+            qid[i] = (d & 1) ? -1 : 0;
+            cnt += (d & 1) ? 0 : 1;
+        }
+        const int ln = tid & 63, wv = tid >> 6;
+        int inc = cnt;                                         // inclusive scan over the wave
+        for (int o = 1; o < 64; o <<= 1) { const int v = __shfl_up(inc, o); if (ln >= o) inc += v; }
+        if (ln == 63) wsum[wv] = inc;
+        __syncthreads();
+        int base = inc - cnt;
+        for (int w = 0; w < wv; w++) base += wsum[w];
+        for (int i = b0; i < b1; i++) if (qid[i] == 0) qid[i] = base++;
+        __syncthreads();
+        float4* qn = A.fnode + 4 * (size_t)m;
+        for (int i = tid; i < m; i += nt) {
+            if (qid[i] < 0) continue;
+            float* q = reinterpret_cast<float*>(qn + 7 * (size_t)qid[i]);
+            int* qr = reinterpret_cast<int*>(qn + 7 * (size_t)qid[i] + 6);
+            const float* bi = reinterpret_cast<const float*>(A.fnode + 4 * (size_t)i);
+            for (int c = 0; c < 2; c++) {                      // child A -> slots 0, 1; B -> 2, 3
+                const int ch = bref(i, c);
+                float* qp = q + 12 * c;
+                for (int s = 0; s < 2; s++) {
+                    const float* src;                          // binary record and side of the slot's box
+                    int side, ref;
+                    if (ch >= 0) { src = reinterpret_cast<const float*>(A.fnode + 4 * (size_t)ch); side = s; ref = bref(ch, s); }
+                    else { src = bi; side = c; ref = s == 0 ? ch : QEMPTY; }   // a leaf child: itself, then empty
+                    for (int k = 0; k < 6; k++) qp[2 * k + s] = src[2 * k + side];
+                    qr[2 * c + s] = ref >= 0 ? qid[ref] : ref;
+                }
+            }
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2272,7 +2421,7 @@ struct rt_scene {
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
     DLight* d_lights = nullptr; Box* d_mesh_box = nullptr; Box* d_tree = nullptr;
     float4* d_node_pair = nullptr; int* d_leaf = nullptr;
-    float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
+    float4* d_fnode = nullptr; int n_real = 0, fdepth = 0, n_quad = 0;   // ordered LBVH (fast kernel) + quad records
     float4* d_inst4 = nullptr;
     TriAx* d_tri_ax = nullptr;                   // axis-plane triangle records (tri_axis_records)
     int* d_work = nullptr; int n_cu = 0;
@@ -2459,8 +2608,11 @@ std::vector<Box> mesh_boxes(const rt::Scene& h) {
     }
     return mbox;
 }
-void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
+// n_real, the deepest internal node's depth (root = 1) and the number of quad records
+// (RT_QUAD: internal nodes at odd depth here, i.e. even from a root at 0).
+void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth, int* n_quad) {
     const std::vector<Box> mbox = mesh_boxes(h);
+    *n_quad = 0;
     std::vector<std::pair<unsigned long long, int>> kv;
     bool ordered = true;                                      // every real box finite with mn <= mx
     for (size_t i = 0; i < h.d_insts.size(); i++) {
@@ -2495,6 +2647,7 @@ void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
         const auto [node, d] = todo.back();
         todo.pop_back();
         *depth = std::max(*depth, d);
+        *n_quad += d & 1;
         if (d > nr) { *depth = 1 << 20; return; }          // malformed: disable the fast tree
         for (int c = 0; c < 2; c++) if (child[2 * node + c] >= 0) todo.push_back({child[2 * node + c], d + 1});
     }
@@ -2538,9 +2691,9 @@ int upload(rt_scene* s) {
     s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
     HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
-    ordered_tree_shape(h, &s->n_real, &s->fdepth);
+    ordered_tree_shape(h, &s->n_real, &s->fdepth, &s->n_quad);
     s->shape_gen = s->inst_gen;
-    HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
+    HIPCHK(hipMalloc((void**)&s->d_fnode, (RT_QUAD ? 11 : 4) * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));   // binary (+ quad)
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_work, WORK_INTS * sizeof(int)));
@@ -2604,7 +2757,7 @@ int sync_slot_insts(rt_scene* s, hipStream_t st) {
 void refresh_shape(rt_scene* s) {
     if (s->shape_gen == s->inst_gen) return;
     int nr = 0;
-    ordered_tree_shape(s->h, &nr, &s->fdepth);
+    ordered_tree_shape(s->h, &nr, &s->fdepth, &s->n_quad);
     s->shape_gen = s->inst_gen;
 }
 
@@ -2630,7 +2783,7 @@ int ensure_other_slot(rt_scene* s) {
         rt_scene::Slot& o = s->store[i];
         if (i == s->cur_slot || o.d_work) continue;
         HIPCHK(hipMalloc((void**)&o.d_node_pair, 3 * nl * sizeof(float4)));
-        HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
+        HIPCHK(hipMalloc((void**)&o.d_fnode, (RT_QUAD ? 11 : 4) * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));   // binary (+ quad)
         HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
         HIPCHK(hipMalloc((void**)&o.d_work, WORK_INTS * sizeof(int)));
@@ -2743,7 +2896,7 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     SceneView v;
     v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
     v.node_pair = s->d_node_pair; v.leaf_inst = s->d_leaf;
-    v.fnode = s->d_fnode; v.n_real = s->n_real;
+    v.fnode = s->d_fnode; v.n_real = s->n_real; v.n_quad = s->n_quad;
 #ifndef RT_NO_FTREE
 #define RT_NO_FTREE 0        // 1: profiling variant, the fast kernel walks the reference heap
 #endif
