@@ -216,6 +216,9 @@ struct BvhRefs {
 #ifndef RT_UNLIT_SKIP
 #define RT_UNLIT_SKIP 1      // fast frames skip shadow rays of lights with a zero phong factor
 #endif
+#ifndef RT_SKY_REP
+#define RT_SKY_REP 1         // sky_kernel: an undecided group whose representative primary enters the root is live
+#endif
 #ifndef RT_SKY_PERRAY
 #define RT_SKY_PERRAY 1      // sky_kernel runs the exact per-ray test on groups the cone test leaves
 #endif
@@ -1880,7 +1883,20 @@ __global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, un
         const int gl = base + lane;
         const bool in = lane < n_in;
         const bool csky = in && RT_SKY_CONE && cone_misses_root(P, S, gl);
-        const unsigned long long m = __ballot(csky), t = __ballot(in && !csky);
+        // Representative ray (RT_SKY_REP): a group the cone test leaves undecided is live as
+        // soon as one of its primaries enters the root -- lane 0's (pixel 0, sample 0), the
+        // trace kernel's own ray and test -- so only the groups whose representative misses
+        // need the 64-ray test below.  One group per lane here.
+        bool rlive = false;
+        if (RT_SKY_REP && !RT_EXP_SKYCMP && in && !csky) {
+            const int gy = (int)udiv((unsigned)gl, P.div_ngx), gx = gl - gy * P.n_gx;
+            const float2 o = P.spp_off[0];
+            const Ray rr = camera_at(P.cam, (float)(gx * P.gw) + o.x, (float)(P.row0 + gy * P.gh * P.row_step) + o.y);
+            BvhRefs bv{};
+            bv.fnode = S.fnode;
+            rlive = ft_root_hit(S, bv, true, rr);
+        }
+        const unsigned long long m = __ballot(csky), t = __ballot(in && !csky && !rlive);
         if (csky) {
             gsky[gl] = 1;
             // the trace kernel records (hf_next) only the groups it runs: a sky group's entry
@@ -1888,6 +1904,13 @@ __global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, un
             if (P.hist) P.hf_next[gl] = 0;
         }
         if (lane == 0) { s_sky = m; s_todo = t; s_cnt = 0; }
+        if (rlive) gsky[gl] = 0;
+        const unsigned long long rl = __ballot(rlive);
+        if (rl) {                                              // live already: into the block's list
+            const int pos = __popcll(rl & ((1ull << lane) - 1ull));
+            if (rlive) s_list[pos] = gl;
+            if (lane == 0) s_cnt = __popcll(rl);
+        }
     }
     __syncthreads();
     auto sky_pixel = [&](int g, int pix) {                     // pixel pix of sky group g: zeros, -1 hit ids
