@@ -1873,7 +1873,11 @@ __device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const Sce
 // appended to list (block % NQ) with one atomic.  Small blocks keep ~8 per CU resident: the
 // per-ray tests are latency-bound chains (measured: 1024-group blocks, 102 -> 71 us per
 // 1080p frame; per-ray tests of every group, 108 us).
-__global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
+#ifndef RT_SKY_WAVES
+#define RT_SKY_WAVES 4       // waves per sky_kernel block (64 groups per block)
+#endif
+constexpr int SKY_THREADS = 64 * RT_SKY_WAVES;
+__global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
     __shared__ unsigned long long s_sky, s_todo;
     __shared__ int s_cnt, s_base, s_list[64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, L = P.lanes_per_px;
@@ -1927,7 +1931,7 @@ __global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, un
     };
     const unsigned long long skym = s_sky;
     if (!RT_EXP_SKYCMP && skym)
-        for (int i = threadIdx.x; i < 64 * P.px_per_wave; i += 256) {
+        for (int i = threadIdx.x; i < 64 * P.px_per_wave; i += SKY_THREADS) {
             const int gi = i / P.px_per_wave;
             if ((skym >> gi) & 1) sky_pixel(base + gi, i - gi * P.px_per_wave);
         }
@@ -1945,7 +1949,7 @@ __global__ __launch_bounds__(256) void sky_kernel(TraceParams P, SceneView S, un
     for (int k = 0; todo; k++) {
         const int bit = __builtin_ctzll(todo);
         todo &= todo - 1;
-        if ((k & 3) != wv) continue;
+        if ((k % RT_SKY_WAVES) != wv) continue;
         const int g = base + bit;
         const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
         const int px = gx * P.gw + pxo, pr = gy * P.gh + pyo;
@@ -3116,7 +3120,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         P.live = RT_EXP_SKYCMP ? nullptr : s->d_live; P.live_cap = lcap;
         if (P.live) P.tpc = RT_TPC_LIVE;
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
-        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(256), sargs, 0, st, e0, nullptr, 0));
+        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
     }
     void* args[] = {&P, &S};
     HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));
