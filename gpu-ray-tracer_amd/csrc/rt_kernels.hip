@@ -251,7 +251,7 @@ constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
 #define RT_QUAD 0            // 1: A/B variant, fast traversal over 4-wide records (bvh_build_kernel's quad
                              // phase): bit-exact (69 GPU tests) but +5% frame (profiles/r02/ab_quad.log)
 #endif
-constexpr int QEMPTY = (int)0x80000000;   // empty slot of a quad record
+[[maybe_unused]] constexpr int QEMPTY = (int)0x80000000;   // empty slot of a quad record
 #ifndef RT_TRAV2
 #define RT_TRAV2 1           // compact fast-traversal step (closest_hit); 0: the previous step, A/B
 #endif
