@@ -2486,7 +2486,10 @@ struct rt_scene {
     unsigned slot_inst_gen = 0;                  // instance generation the current slot's arrays hold
     unsigned inst_gen = 1;                       // generation of the host instance array (set_trans bumps it)
     unsigned shape_gen = 0;                      // generation n_real / fdepth were computed for
-    static constexpr int MAX_SLOTS = 4;
+#ifndef RT_MAX_SLOTS
+#define RT_MAX_SLOTS 4
+#endif
+    static constexpr int MAX_SLOTS = RT_MAX_SLOTS;
     struct Slot {
         Box* d_tree = nullptr; float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_fnode = nullptr;
         int* d_work = nullptr; bool work_zeroed = false, bvh_valid = false;
@@ -3552,7 +3555,7 @@ int rt_exp_build_stamps(unsigned long long* out) {
 
 int rt_scene_set_frame_slots(rt_scene* s, int n) {
     CHECK_FINISHED(s);
-    if (n < 1 || n > rt_scene::MAX_SLOTS) return fail(RT_ERR_ARG, "frame slots: 1 to 4");
+    if (n < 1 || n > rt_scene::MAX_SLOTS) return fail(RT_ERR_ARG, "frame slots: 1 to " + std::to_string(rt_scene::MAX_SLOTS));
     if (n == s->n_slots) return RT_OK;
     if (s->uploaded) { HIPCHK(hipSetDevice(s->device)); HIPCHK(hipDeviceSynchronize()); }   // nothing in flight
     select_slot(s, 0);
