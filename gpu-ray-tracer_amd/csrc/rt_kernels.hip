@@ -118,7 +118,6 @@ struct SceneView {           // read-only scene data (HBM, L2-resident)
     const float4* node_pair;  // BVH child pairs, heap order (written by bvh_build_kernel), see BvhRefs
     const float4* fnode;      // ordered LBVH of the fast kernel (bvh_build_kernel)
     int n_real, ftree;        // its leaf count; 1 if usable (>= 2 leaves, depth <= 31)
-    int n_quad;               // RT_QUAD: its 4-wide records (binary nodes at even depth), after the binary ones
     const int* leaf_inst;
     const float4* inst4;      // compact instance records
     int n_leaf, n_inst, n_lights, use_bvh;
@@ -154,23 +153,6 @@ __device__ __forceinline__ TriRest ld_rest(const DTri* T, int t) {
     return ldc(reinterpret_cast<const TriRest*>(reinterpret_cast<const char*>(T + t) + 24), 0);
 }
 
-// Triangle test of Triangle::hit (geometry.h:273-290) fused with TriInner::tri_hit's
-// acceptance (trimesh.cu:56: time >= 1e-5 && time < isect.time).  The acceptance
-// bound is checked right after the plane intersection — before the barycentric
-// lengths — which changes nothing observable: a rejected triangle has no effect.
-__device__ __forceinline__ bool tri_accept(const DTri& T, const Ray& r, float best, float& time, float& u, float& v) {
-    float denom = dot(r.d, T.pn);
-    if (fabsf(denom) < THRESH) return false;
-    float t = (1.0f / denom) * dot(T.a - r.o, T.pn);
-    if (!(t >= THRESH && t < best)) return false;
-    V3 p = at(r, t);
-    float b0 = len(cross(T.c - p, T.b - p)) / T.area;
-    float b1 = len(cross(T.c - p, T.a - p)) / T.area;
-    float b2 = len(cross(T.a - p, T.b - p)) / T.area;
-    if (fabsf(b0 + b1 + b2 - 1.0f) <= THRESH) { time = t; u = b1; v = b2; return true; }
-    return false;
-}
-
 // BVH nodes and instance records as the trace kernel reads them: from LDS (staged
 // once per persistent block) or, for scenes too large for LDS, from global memory.
 // Nodes are stored by child pair: pair k holds heap nodes 2k (.x lanes) and 2k+1 (.y
@@ -192,44 +174,9 @@ struct BvhRefs {
     const DMesh* meshes;
 };
 
-#ifndef RT_EXP_NORED
-#define RT_EXP_NORED 0       // experiment builds only (group-overhead dissection), see tools/ab.sh
-#endif
-#ifndef RT_EXP_NOHIST
-#define RT_EXP_NOHIST 0
-#endif
-#ifndef RT_EXP_NOCHECK
-#define RT_EXP_NOCHECK 0     // experiment: heavy groups not skipped in the normal queues (run twice)
-#endif
-#ifndef RT_EXP_SKYCMP
-#define RT_EXP_SKYCMP 0      // experiment: trace kernel runs its own sky test and marks disagreements
-#endif
-#ifndef RT_EXP_GLC
-#define RT_EXP_GLC 0
-#endif
-#ifndef RT_SKY_PREPASS
-#define RT_SKY_PREPASS 1     // sky groups decided and written by sky_kernel before the trace kernel
-#endif
-#ifndef RT_SKY_CONE
-#define RT_SKY_CONE 1        // sky_kernel decides groups by their ray cone first (cone_misses_root)
-#endif
-#ifndef RT_UNLIT_SKIP
-#define RT_UNLIT_SKIP 1      // fast frames skip shadow rays of lights with a zero phong factor
-#endif
-#ifndef RT_SKY_REP
-#define RT_SKY_REP 1         // sky_kernel: an undecided group whose representative primary enters the root is live
-#endif
-#ifndef RT_SKY_PERRAY
-#define RT_SKY_PERRAY 1      // sky_kernel runs the exact per-ray test on groups the cone test leaves
-#endif
+// Tuning parameters (build switches; the A/B logs under profiles/ record the values tried).
 #ifndef RT_HIST_GROUPS_PER_WAVE
 #define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
-#endif
-#ifndef RT_EXP_NOREC
-#define RT_EXP_NOREC 0       // experiment: no duration recording (the history stays the first frame's)
-#endif
-#ifndef RT_FILTERED
-#define RT_FILTERED 1        // 0: always the exact reference arithmetic (A/B and validation)
 #endif
 #ifndef RT_TPC
 #define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop) over all
@@ -240,34 +187,17 @@ struct BvhRefs {
                              // wave, one per ticket balances them (profiles/r02/sky_live_tpc.log)
 #endif
 constexpr int TPC = RT_TPC;
-#ifndef RT_SHADE_LDS
-#define RT_SHADE_LDS 1       // materials, lights, triangles and meshes copied into LDS (M_SHADE kernels)
-#endif
-#ifndef RT_ZERO_AXIS_CUT
-#define RT_ZERO_AXIS_CUT 1   // 0: A/B variant, zero-direction axes unconstrained as in the reference (closest_hit)
-#endif
-constexpr bool ZERO_AXIS_CUT = RT_ZERO_AXIS_CUT != 0;
-#ifndef RT_QUAD
-#define RT_QUAD 0            // 1: A/B variant, fast traversal over 4-wide records (bvh_build_kernel's quad
-                             // phase): bit-exact (69 GPU tests) but +5% frame (profiles/r02/ab_quad.log)
-#endif
-[[maybe_unused]] constexpr int QEMPTY = (int)0x80000000;   // empty slot of a quad record
-#ifndef RT_TRAV2
-#define RT_TRAV2 1           // compact fast-traversal step (closest_hit); 0: the previous step, A/B
-#endif
-#ifndef RT_ANYASM
-#define RT_ANYASM 2          // 1: the step's two wave hits as 0/1 SGPR integers (any_lane); 2: also the
-                             // exact-fallback test (same-box A/B, profiles/r02/ab_anyasm.log: 0.806 -> 0.797 ms)
-#endif
-#ifndef RT_PK_PAIR
-#define RT_PK_PAIR 0         // 1: A/B variant, child-pair slabs in packed (v_pk_*) f32 arithmetic; the splat
-                             //    copies it needs cost ~30 VGPRs, which at 128 VGPRs/lane (4 waves/SIMD) is a loss
-#endif
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 splat(float x) { return f2{x, x}; }
-__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return f2{fminf(a.x, b.x), fminf(a.y, b.y)}; }
-__device__ __forceinline__ f2 vmax(f2 a, f2 b) { return f2{fmaxf(a.x, b.x), fmaxf(a.y, b.y)}; }
+// One child box's slab interval [lo, hi] against a ray through its reciprocals (ray_inv):
+// fma(m - o, 1/d, -+bias) per face, the bias carrying the zero-direction skip (ray_inv).
+__device__ __forceinline__ void slab(const Ray& r, const RayInv& ri, float mnx, float mny, float mnz, float mxx,
+                                     float mxy, float mxz, float& lo, float& hi) {
+    const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
+    const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
+    const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
+    lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
+    hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
+}
 
 // BoundingBox::intersects (bounding_box.cu:62-104) for both children of pair k.
 // Filtered like box_hit_f (rt_math.h), with the bound taken from the slab results
@@ -282,34 +212,9 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
                                             bool& h0, bool& h1, float& t0, float& t1) {
     const float4 A = rec[0], B = rec[1], C = rec[2];
     const bool nd0 = A.x <= B.z, nd1 = A.y <= B.w;            // nondegenerate (bounding_box.cu:63-65)
-    t0 = -INFINITY; t1 = -INFINITY;
-    auto exact = [&](int c) {
-        return c == 0 ? box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) : box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r);
-    };
-#if RT_FILTERED && !RT_PK_PAIR
-    // per-child f32 slabs (no splat register copies; see RT_PK_PAIR)
-    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
-        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
-        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
-        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
-        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
-        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
-    };
     float lo0, hi0, lo1, hi1;
-    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
-    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
-    const f2 lo{lo0, lo1}, hi{hi0, hi1};
-#elif RT_FILTERED
-    const f2 mnx{A.x, A.y}, mny{A.z, A.w}, mnz{B.x, B.y}, mxx{B.z, B.w}, mxy{C.x, C.y}, mxz{C.z, C.w};
-    const f2 ix = splat(ri.ix), iy = splat(ri.iy), iz = splat(ri.iz);
-    const f2 bx = splat(ri.bx), by = splat(ri.by), bz = splat(ri.bz);
-    const f2 qx0 = __builtin_elementwise_fma(mnx - splat(r.o.x), ix, -bx), qx1 = __builtin_elementwise_fma(mxx - splat(r.o.x), ix, bx);
-    const f2 qy0 = __builtin_elementwise_fma(mny - splat(r.o.y), iy, -by), qy1 = __builtin_elementwise_fma(mxy - splat(r.o.y), iy, by);
-    const f2 qz0 = __builtin_elementwise_fma(mnz - splat(r.o.z), iz, -bz), qz1 = __builtin_elementwise_fma(mxz - splat(r.o.z), iz, bz);
-    const f2 lo = vmax(vmax(vmin(qx0, qx1), vmin(qy0, qy1)), vmin(qz0, qz1));
-    const f2 hi = vmin(vmin(vmax(qx0, qx1), vmax(qy0, qy1)), vmax(qz0, qz1));
-#endif
-#if RT_FILTERED
+    slab(r, ri, A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(r, ri, A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
     // Certain outcomes (the exact reference result known): with el, eh the error margins of
     // lo, hi, c = lo + el and a = hi - eh bound the reference's tmin from above and its tmax
     // from below, so max(c, 1e-5) <= a is certainly a hit; with d = lo - el, b = hi + eh,
@@ -317,64 +222,21 @@ __device__ __forceinline__ void pair_hit_at(const float4* rec, const Ray& r, con
     // For filtered rays lo and hi are finite (ray_inv sends a direction without a nonzero
     // component to the exact test), so the max forms equal the pairs of comparisons.
     // Lanes in between run the exact reference test; one uniform branch for both children.
-    const f2 el{fmaf(fabsf(lo.x), FILT_BOX, FILT_ABS), fmaf(fabsf(lo.y), FILT_BOX, FILT_ABS)};
-    const f2 eh{fmaf(fabsf(hi.x), FILT_BOX, FILT_ABS), fmaf(fabsf(hi.y), FILT_BOX, FILT_ABS)};
-    const f2 cc = lo + el, aa = hi - eh, dd = lo - el, bb = hi + eh;
+    const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS);
+    const float eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
+    const float d0 = lo0 - el0, d1 = lo1 - el1;
     const bool fx = active && !ri.exact;
-    const bool c0 = fx && nd0 && fmaxf(cc.x, THRESH) <= aa.x;
-    const bool c1 = fx && nd1 && fmaxf(cc.y, THRESH) <= aa.y;
-    const bool m0 = !nd0 || (fx && fmaxf(dd.x, THRESH) > bb.x);
-    const bool m1 = !nd1 || (fx && fmaxf(dd.y, THRESH) > bb.y);
+    const bool c0 = fx && nd0 && fmaxf(lo0 + el0, THRESH) <= hi0 - eh0;
+    const bool c1 = fx && nd1 && fmaxf(lo1 + el1, THRESH) <= hi1 - eh1;
+    const bool m0 = !nd0 || (fx && fmaxf(d0, THRESH) > hi0 + eh0);
+    const bool m1 = !nd1 || (fx && fmaxf(d1, THRESH) > hi1 + eh1);
     h0 = c0; h1 = c1;
-    t0 = c0 ? dd.x : -INFINITY;
-    t1 = c1 ? dd.y : -INFINITY;
+    t0 = c0 ? d0 : -INFINITY;
+    t1 = c1 ? d1 : -INFINITY;
     const bool x0 = active && !m0 && !c0, x1 = active && !m1 && !c1;
     if (__builtin_expect(__ballot(x0 || x1) != 0, 0)) {
-        if (x0) h0 = exact(0);
-        if (x1) h1 = exact(1);
-    }
-#else
-    h0 = active && nd0 && exact(0);
-    h1 = active && nd1 && exact(1);
-#endif
-}
-// pair_hit_at for the fast traversal, with each child's result as one float: the entry
-// lower bound (lo - el, or -inf after the exact test) for a hit, NaN for a miss.  Certain
-// outcomes and the exact fallback as in pair_hit_at; the filtered-ray condition is folded
-// into the masks so no boolean is materialised.
-__device__ __forceinline__ void pair_hit_tt(const float4* rec, const Ray& r, const RayInv& ri, bool active,
-                                            float& ta, float& tb) {
-    const float4 A = rec[0], B = rec[1], C = rec[2];
-    const bool nd0 = A.x <= B.z, nd1 = A.y <= B.w;            // nondegenerate (bounding_box.cu:63-65)
-#if !RT_FILTERED
-    ta = active && nd0 && box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : __builtin_nanf("");
-    tb = active && nd1 && box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : __builtin_nanf("");
-    return;
-#endif
-    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
-        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
-        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
-        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
-        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
-        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
-    };
-    float lo0, hi0, lo1, hi1;
-    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
-    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
-    const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS);
-    const float el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
-    const float d0 = lo0 - el0, d1 = lo1 - el1;
-    const bool hc0 = fmaxf(lo0 + el0, THRESH) <= hi0 - eh0, hc1 = fmaxf(lo1 + el1, THRESH) <= hi1 - eh1;
-    const bool mc0 = fmaxf(d0, THRESH) > hi0 + eh0, mc1 = fmaxf(d1, THRESH) > hi1 + eh1;
-    const bool fx = active && !ri.exact;
-    const float QNAN = __builtin_nanf("");
-    ta = (fx && nd0 && hc0) ? d0 : QNAN;
-    tb = (fx && nd1 && hc1) ? d1 : QNAN;
-    const bool x0 = active && nd0 && (ri.exact || !(hc0 || mc0));
-    const bool x1 = active && nd1 && (ri.exact || !(hc1 || mc1));
-    if (__builtin_expect(__ballot(x0 || x1) != 0, 0)) {
-        if (x0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
-        if (x1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
+        if (x0) h0 = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r);
+        if (x1) h1 = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r);
     }
 }
 // 0/1 in an SGPR from a wave mask, opaque to the optimizer (a boolean taken from a ballot is
@@ -384,25 +246,20 @@ __device__ __forceinline__ unsigned any_lane(unsigned long long m) {
     asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(h) : "s"(m) : "scc");
     return h;
 }
-// pair_hit_tt for the compact traversal step (RT_TRAV2).  Every record of the ordered tree is a
-// proper finite box (the host leaves a frame with a degenerate or non-finite real box to the heap
-// kernels: ordered_tree_shape), so there is no per-child degenerate test; a ray that needs the
-// exact test everywhere (ri.exact) enters with NaN reciprocals (closest_hit), so both its slab
-// results are NaN and both outcome tests are false: it takes the exact test with no filtered-ray
-// mask.  ta/tb carry no activity mask: an inactive lane's cut is NaN, so t <= cut is false for it.
+// pair_hit_at for the fast traversal step, with each child's result as one float: the entry
+// lower bound (lo - el, or -inf after the exact test) for a hit, NaN for a miss.  Every record
+// of the ordered tree is a proper finite box (the host leaves a frame with a degenerate or
+// non-finite real box to the heap kernels: ordered_tree_shape), so there is no per-child
+// degenerate test; a ray that needs the exact test everywhere (ri.exact) enters with NaN
+// reciprocals (closest_hit), so both its slab results are NaN and both outcome tests are
+// false: it takes the exact test with no filtered-ray mask.  ta/tb carry no activity mask: an
+// inactive lane's cut is NaN, so t <= cut is false for it.
 __device__ __forceinline__ void pair_hit_tt2(const float4* rec, const Ray& r, const RayInv& ri, bool active,
                                              float& ta, float& tb) {
     const float4 A = rec[0], B = rec[1], C = rec[2];
-    auto slab = [&](float mnx, float mny, float mnz, float mxx, float mxy, float mxz, float& lo, float& hi) {
-        const float qx0 = fmaf(mnx - r.o.x, ri.ix, -ri.bx), qx1 = fmaf(mxx - r.o.x, ri.ix, ri.bx);
-        const float qy0 = fmaf(mny - r.o.y, ri.iy, -ri.by), qy1 = fmaf(mxy - r.o.y, ri.iy, ri.by);
-        const float qz0 = fmaf(mnz - r.o.z, ri.iz, -ri.bz), qz1 = fmaf(mxz - r.o.z, ri.iz, ri.bz);
-        lo = fmaxf(fmaxf(fminf(qx0, qx1), fminf(qy0, qy1)), fminf(qz0, qz1));
-        hi = fminf(fminf(fmaxf(qx0, qx1), fmaxf(qy0, qy1)), fmaxf(qz0, qz1));
-    };
     float lo0, hi0, lo1, hi1;
-    slab(A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
-    slab(A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
+    slab(r, ri, A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(r, ri, A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
     const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS);
     const float el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
     const float d0 = lo0 - el0, d1 = lo1 - el1;
@@ -412,11 +269,7 @@ __device__ __forceinline__ void pair_hit_tt2(const float4* rec, const Ray& r, co
     ta = hc0 ? d0 : QNAN;
     tb = hc1 ? d1 : QNAN;
     const bool k0 = hc0 || mc0, k1 = hc1 || mc1;               // outcome certain
-#if RT_ANYASM >= 2
     if (__builtin_expect(any_lane(__ballot(active && !(k0 && k1))), 0)) {
-#else
-    if (__builtin_expect(__ballot(active && !(k0 && k1)) != 0, 0)) {
-#endif
         if (active && !k0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
         if (active && !k1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
     }
@@ -433,26 +286,6 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
-#ifndef RT_EXP_PAD
-#define RT_EXP_PAD 0         // experiment builds: sensitivity probe, RT_EXP_PAD dummy VALU at site RT_EXP_PAD_SITE
-#define RT_EXP_PAD_SITE 0
-#endif
-template <int SITE> __device__ __forceinline__ void exp_pad() {
-#if RT_EXP_PAD
-    if (SITE == RT_EXP_PAD_SITE) {
-        int x = 0;
-#pragma unroll
-#if RT_EXP_PAD_SALU
-        for (int i = 0; i < RT_EXP_PAD; i++) asm volatile("s_add_u32 %0, 1, %0" : "+s"(x));
-        asm volatile("" :: "s"(x));
-#else
-        for (int i = 0; i < RT_EXP_PAD; i++) asm volatile("v_add_u32 %0, 1, %0" : "+v"(x));
-        asm volatile("" :: "v"(x));
-#endif
-    }
-#endif
-}
-
 __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
     const float4 I = bv.inst[ti];
     const int w = __float_as_int(I.w);
@@ -517,7 +350,6 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
     }
     int best = -1;
     float bu = 0.0f, bv_ = 0.0f, t_best = b.time;
-#if RT_FILTERED
     if (AXIS) {
         // Axis-plane path (fast kernel, identity rotations): exact plane time from the
         // per-query reciprocal (axis_plane_t), then the exact in-plane reject (TriAx);
@@ -578,13 +410,6 @@ __device__ __forceinline__ bool cast_local(const SceneView& S, const BvhRefs& bv
             t_best = time; best = t; bu = u; bv_ = v;
         }
     }
-#else
-    for (int t = mesh.tri_begin; t < mesh.tri_begin + mesh.tri_count; t++) {
-        const DTri T = ldc(S.tris, t);
-        float time, u, v;
-        if (tri_accept(T, mr, t_best, time, u, v)) { t_best = time; best = t; bu = u; bv_ = v; }
-    }
-#endif
     if (best < 0) return false;
     b.time = (t_best * scale) * dir_len;                      // fix_isect, then cast_local
     b.inst = ti; b.tri = best; b.u = bu; b.v = bv_;
@@ -619,7 +444,7 @@ __device__ __forceinline__ V3 hit_normal(const SceneView& S, const BvhRefs& bv, 
 // time, so entry bounds stay valid).  closest_hit's `im` keeps the nonzero axes only.
 // Fast (ordered-LBVH) kernels only.
 __device__ __forceinline__ void zero_axis_cut(const SceneView& S, const Ray& r, RayInv& ri) {
-    if (!ZERO_AXIS_CUT || !(S.prune_abs >= 0.0f)) return;
+    if (!(S.prune_abs >= 0.0f)) return;
     constexpr float K = 0x1p32f;
     if (r.d.x == 0.0f) { ri.ix = K; ri.bx = K * S.prune_abs; }
     if (r.d.y == 0.0f) { ri.iy = K; ri.by = K * S.prune_abs; }
@@ -634,7 +459,7 @@ __device__ __forceinline__ bool ft_root_hit(const SceneView& S, const BvhRefs& b
     zero_axis_cut(S, r, ri);
     bool h0, h1;
     float t0, t1;
-    pair_hit_at(RT_QUAD ? S.fnode : bv.fnode, r, ri, active, h0, h1, t0, t1);   // the binary root record
+    pair_hit_at(bv.fnode, r, ri, active, h0, h1, t0, t1);     // the root record
     return h0 || h1;
 }
 
@@ -676,10 +501,7 @@ template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false, bool PROF
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
-#ifndef RT_NOPRUNE
-#define RT_NOPRUNE 0         // 1: profiling variant without distance pruning
-#endif
-    const bool prune = !RT_NOPRUNE && !STATS && S.prune_abs >= 0.0f;
+    const bool prune = !STATS && S.prune_abs >= 0.0f;
     float im = 0.0f;                                           // max_a |1/d_a| (set below)
     auto slack = [&](float t) { return (S.prune_abs + 0x1p-14f * fabsf(t)) * im + 0x1p-14f * fabsf(t); };
     auto cut = [&]() {
@@ -732,7 +554,6 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         // leaf improves the closest hit: recomputed after each leaf visit, not every step.
         const float QNAN = __builtin_nanf("");
         float ct = !active_in ? QNAN : prune ? cut() : INFINITY;
-#if RT_TRAV2
         // Compact step (same visits, same order), one loop latch: a step either descends into
         // A (B pushed when hit) or runs up to two leaves at the single leaf site (A then B) and
         // continues at an internal B or pops.  A popped "leaf B of node X" re-runs X's pair test
@@ -742,91 +563,9 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
         if (ri.exact) ri.ix = ri.iy = ri.iz = QNAN;           // every box: the exact test (pair_hit_tt2)
         int node = 0, sp = 0, stk = 0, bonly = 0;
         auto push = [&](int e) { asm("v_writelane_b32 %0, %1, m0" : "+v"(stk) : "s"(e), "{m0}"(sp)); sp++; };
-#if RT_QUAD
-        // 4-wide step (bvh_build_kernel's quad records): the four slots (A's children or A, then
-        // B's) are tested in one LDS round trip; hit leaves before the first hit internal slot run
-        // now, in slot order, at the single leaf site; the first hit internal slot is the next
-        // node; hit slots after it are pushed in reverse order (a leaf as -2 - (4 node + slot),
-        // re-tested when popped: bonly = slot + 1).  Same leaves, same order as the binary walk.
-        // The stack holds <= 3 entries per quad level: <= 48 for binary depth <= 31 (host check).
-        (void)bonly;
-        int pslot = -1;                                        // popped leaf entry: its slot
-        // guards against malformed records (never taken on a tree the build kernel wrote): every
-        // wave leaves the loop within 2^16 steps, leaf ids outside the instance range are skipped
-        for (int guard = 0; guard < (1 << 16); guard++) {
-            const float4* rec = bv.fnode + 7 * node;
-            if (PROF) wc.wpair++;
-            exp_pad<1>();                                      // experiment: per step
-            const int4 rf = *reinterpret_cast<const int4*>(rec + 6);
-            const int r0 = uni(rf.x), r1 = uni(rf.y), r2 = uni(rf.z), r3 = uni(rf.w);
-            float t0, t1, t2, t3;
-            unsigned lv, nxt_bit = 0;                          // slots to run at the leaf site now
-            int next = -1;
-            if (pslot >= 0) {                                  // popped leaf: its pair only
-                const int ps = pslot;
-                pslot = -1;
-                float ta, tb;
-                pair_hit_tt2(rec + 3 * (ps >> 1), r, ri, ct == ct, ta, tb);
-                t0 = t1 = t2 = t3 = (ps & 1) ? tb : ta;        // (only slot ps is read)
-                lv = 1u << ps;
-            } else {
-                pair_hit_tt2(rec, r, ri, ct == ct, t0, t1);
-                pair_hit_tt2(rec + 3, r, ri, ct == ct, t2, t3);
-                const unsigned h = (any_lane(__ballot(t0 <= ct)) & (unsigned)(r0 != QEMPTY)) |
-                                   ((any_lane(__ballot(t1 <= ct)) & (unsigned)(r1 != QEMPTY)) << 1) |
-                                   ((any_lane(__ballot(t2 <= ct)) & (unsigned)(r2 != QEMPTY)) << 2) |
-                                   ((any_lane(__ballot(t3 <= ct)) & (unsigned)(r3 != QEMPTY)) << 3);
-                const unsigned im = (unsigned)(r0 >= 0) | ((unsigned)(r1 >= 0) << 1) | ((unsigned)(r2 >= 0) << 2) |
-                                    ((unsigned)(r3 >= 0) << 3);
-                const unsigned hi = h & im;
-                const int f = hi ? __builtin_ctz(hi) : 4;      // first hit internal slot
-                lv = h & ((1u << f) - 1u);                     // hit leaves before it
-                if (f < 4) {
-                    next = f == 0 ? r0 : f == 1 ? r1 : f == 2 ? r2 : r3;
-                    nxt_bit = h & ~((2u << f) - 1u);           // hit slots after it
-                    for (int i = 3; i > f; i--)
-                        if ((nxt_bit >> i) & 1u) {
-                            const int ri_ = i == 1 ? r1 : i == 2 ? r2 : r3;
-                            push(ri_ >= 0 ? ri_ : -2 - (4 * node + i));
-                        }
-                }
-            }
-            while (lv) {                                       // the leaf site, slots in order
-                const int sl = __builtin_ctz(lv);
-                lv &= lv - 1u;
-                const float lt = sl == 0 ? t0 : sl == 1 ? t1 : sl == 2 ? t2 : t3;
-                const int linst = -1 - (sl == 0 ? r0 : sl == 1 ? r1 : sl == 2 ? r2 : r3);
-                if ((unsigned)linst >= (unsigned)S.n_inst) continue;
-                const bool lh = lt <= ct;                      // (ct only decreases)
-                if (__ballot(lh)) {
-                    exp_pad<2>();                              // experiment: per leaf visit
-                    if (!pre_ok) {
-                        if (AXIS) pre = dir_pre<true>(r.d);    // S.tri_ax set: identity rotations
-                        else if (S.ident_all) pre = dir_pre(r.d);
-                        pre_ok = true;
-                    }
-                    const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-                    if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
-                    if (lh && cast_local<false, AXIS, PROF>(S, bv, linst, r, b, pre, wc, t_low(lt)))
-                        if (b.time <= occl_t) ct = QNAN;       // occluded: this lane is done
-                    if (prune && ct == ct) ct = cut();
-                    if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
-                    if (!__ballot(ct == ct)) { next = -1; sp = 0; break; }   // every lane occluded: done
-                }
-            }
-            if (next >= 0) { node = next; continue; }
-            if (sp == 0) break;
-            sp--;                                              // a quad node, or leaf slot s of node n: -2 - (4 n + s)
-            const int e = __builtin_amdgcn_readlane(stk, sp);
-            if (e < 0) { node = (-2 - e) >> 2; pslot = (-2 - e) & 3; }
-            else node = e;
-        }
-        return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
-#endif
         for (;;) {
             const float4* rec = bv.fnode + 4 * node;
             if (PROF) wc.wpair++;
-            exp_pad<1>();                                      // experiment: per child-pair step
             const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
             const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
             float ta, tb;
@@ -837,11 +576,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 bonly = 0;
                 lt = tb; linst = -1 - rb;
             } else {
-#if RT_ANYASM
                 const unsigned hA = any_lane(__ballot(ta <= ct)), hB = any_lane(__ballot(tb <= ct));
-#else
-                const bool hA = __ballot(ta <= ct) != 0, hB = __ballot(tb <= ct) != 0;
-#endif
                 if (ra >= 0 && hA) {                           // descend into A, B after A's subtree
                     next = ra;
                     if (hB) push(rb >= 0 ? rb : -2 - node);
@@ -858,7 +593,6 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
                 for (;;) {                                     // the leaf site: one or two leaves
                     const bool lh = lt <= ct;                  // (ct only decreases: fresh for the second leaf)
                     if (__ballot(lh)) {
-                        exp_pad<2>();                          // experiment: per leaf visit
                         if (!pre_ok) {
                             if (AXIS) pre = dir_pre<true>(r.d);    // S.tri_ax set: identity rotations
                             else if (S.ident_all) pre = dir_pre(r.d);
@@ -884,76 +618,6 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             else node = e;
         }
         return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
-#else
-        int node = 0, sp = 0, stk = 0, bonly = 0, has2 = 0, inst2 = 0;
-        float t2 = QNAN;
-        const int my_lane = __lane_id();
-        auto push = [&](int e) { stk = my_lane == sp ? e : stk; sp++; };   // v_writelane
-        for (;;) {
-            float lt = QNAN;                                   // leaf of this iteration: entry bound / NaN
-            int linst = -1;                                    // its instance (uniform), -1: none
-            if (has2) {                                        // leaf B right after leaf A (fresh cut below)
-                lt = t2; linst = inst2; has2 = 0;
-            } else {
-                const float4* rec = bv.fnode + 4 * node;
-                if (PROF) wc.wpair++;
-                exp_pad<1>();                                  // experiment: per child-pair step
-                // child references first, in the same LDS batch as the boxes: one round trip
-                // per step (read after the pair test, they cost a second dependent one)
-                const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
-                const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
-                float ta, tb;
-                pair_hit_tt(rec, r, ri, ct == ct, ta, tb);
-                const bool bA = __ballot(ta <= ct) != 0, bB = __ballot(tb <= ct) != 0;
-                const int bo = bonly;                          // child B only (popped leaf B)
-                bonly = 0;
-                const bool goA = !bo && ra >= 0 && bA;
-                const bool goB = rb >= 0 && bB;
-                if (!bo && ra < 0) { lt = ta; linst = -1 - ra; }
-                if (rb < 0) {
-                    if (goA) {
-                        if (bB) push(-2 - node);
-                    } else if (linst >= 0) {
-                        t2 = tb; inst2 = -1 - rb; has2 = 1;
-                    } else {
-                        lt = tb; linst = -1 - rb;
-                    }
-                }
-                if (goA) {
-                    if (goB) push(rb);
-                    node = ra;
-                    continue;
-                }
-                if (goB) {
-                    if (linst < 0) { node = rb; continue; }
-                    push(rb);                                  // internal B after leaf A
-                }
-            }
-            const bool lh = lt <= ct;                          // (ct only decreases: a fresh cut for leaf B)
-            if (linst >= 0 && __ballot(lh)) {
-                exp_pad<2>();                                  // experiment: per leaf visit
-                if (!pre_ok) {
-                    if (AXIS) pre = dir_pre<true>(r.d);        // S.tri_ax set: identity rotations
-                    else if (S.ident_all) pre = dir_pre(r.d);
-                    pre_ok = true;
-                }
-                const unsigned long long cl0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-                if (PROF) { wc.wleaf++; wc.leaves += __popcll(__ballot(lh)); }
-                if (lh && cast_local<false, AXIS, PROF>(S, bv, uni(linst), r, b, pre, wc, t_low(lt)))
-                    if (b.time <= occl_t) ct = QNAN;           // occluded: this lane is done
-                if (prune && ct == ct) ct = cut();
-                if (PROF) wc.cyc_leaf += __builtin_amdgcn_s_memtime() - cl0;
-                if (!__ballot(ct == ct)) break;                // every lane occluded
-            }
-            if (has2) continue;
-            if (sp == 0) break;
-            sp--;                                              // pop: an internal node, or leaf B of node -2 - e
-            const int e = __builtin_amdgcn_readlane(stk, sp);
-            if (e < 0) { node = -2 - e; bonly = 1; }
-            else node = e;
-        }
-        return active_in && b.time < INFINITY;                 // an accepted triangle has a finite time
-#endif
     }
     if (STATS) wc.nodes += __popcll(am);                       // root test
     bool hr, hdummy;
@@ -964,10 +628,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     DirPre pre{};
     if (S.ident_all) pre = dir_pre(r.d);
     // lower bound of acceptable local times in a leaf entered at >= tl (see distance pruning)
-#ifndef RT_BOXBOUND_STATS
-#define RT_BOXBOUND_STATS 0  // 1: profiling variant, counted kernels also skip inside tests
-#endif
-    const bool box_bound = (RT_BOXBOUND_STATS || !STATS) && S.prune_abs >= 0.0f;   // counted kernel: plain reference path
+    const bool box_bound = !STATS && S.prune_abs >= 0.0f;   // counted kernel: plain reference path
     auto t_low = [&](float tl) { return box_bound ? tl - slack(tl) : -INFINITY; };
     auto leaf = [&](bool h, int li, float tl) {
         const unsigned long long m = __ballot(h);
@@ -1040,9 +701,6 @@ __device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_
     return diffuse + specular;
 }
 __device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
-#if RT_EXP_NOPHONG                                             // experiment: shading arithmetic priced (wrong colours)
-    return incoming + kd;
-#endif
     return phong_factor(m, kd, nrm, ray_dir, to_light) * incoming;
 }
 
@@ -1357,7 +1015,6 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             dtl.x = get(); dtl.y = get(); dtl.z = get();
         }
         unsigned long long c1 = 0;
-        exp_pad<3>();                                          // experiment: per query
         if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
         if (!need) continue;
         int hmat = 0;
@@ -1437,7 +1094,7 @@ __host__ __device__ inline size_t shade_bytes(const SceneView& S) {
 }
 __host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false) {
     const size_t sh = shade ? shade_bytes(S) : 0;
-    if (ft) return (RT_QUAD ? 112 * (size_t)S.n_quad : 64 * (size_t)(S.n_real - 1)) + 16 * (size_t)S.n_inst + sh;
+    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
     return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
 }
 // word copy of n records of T into LDS at `dst` (block-cooperative)
@@ -1455,7 +1112,7 @@ template <class T> __device__ __forceinline__ const T* stage_words(unsigned char
 template <bool LDS, bool FT = false, bool SHADE = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
-    bv.fnode = RT_QUAD ? S.fnode + 4 * (S.n_real - 1) : S.fnode;   // the traversal's records (quad: after the binary ones)
+    bv.fnode = S.fnode;
     bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
     bv.mats = S.mats; bv.lights = S.lights; bv.tris = S.tris; bv.meshes = S.meshes;
     if (LDS && SHADE) {                                    // after the BVH image (lds_bytes without the cache)
@@ -1466,8 +1123,8 @@ __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* 
         bv.meshes = stage_words(p, S.meshes, S.n_meshes);
     }
     if (LDS && FT) {                                       // ordered LBVH | inst4
-        const int nf = RT_QUAD ? 7 * S.n_quad : 4 * (S.n_real - 1);             // quad records only
-        const float4* src = RT_QUAD ? S.fnode + 4 * (S.n_real - 1) : S.fnode;
+        const int nf = 4 * (S.n_real - 1);
+        const float4* src = S.fnode;
         float4* fn = reinterpret_cast<float4*>(smem);
         float4* in = fn + nf;
         for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = src[i];
@@ -1606,24 +1263,14 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                              : P.live ? live_g()
                              : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)umod((unsigned)ticket * (unsigned)P.scramble)
                                                                          : (int)(((long long)ticket * P.scramble) % per_q));
-#if RT_EXP_GLC
-        auto flag = [&](const unsigned char* f) {
-            uint32_t v;
-            const uint32_t* a = reinterpret_cast<const uint32_t*>(f) + (g >> 2);
-            asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a) : "memory");
-            return (v >> (8 * (g & 3))) & 0xffu;
-        };
-#else
         auto flag = [&](const unsigned char* f) { return (ldc(reinterpret_cast<const uint32_t*>(f), g >> 2) >> (8 * (g & 3))) & 0xffu; };
-#endif
-        if (g >= P.n_groups || (qi < 0 && P.gsky && !RT_EXP_SKYCMP && flag(P.gsky)) ||    // sky group: done by sky_kernel
-            (!RT_EXP_NOCHECK && qi >= 0 && P.hist && flag(P.hf_prev)))
+        if (g >= P.n_groups || (qi < 0 && P.gsky && flag(P.gsky)) ||    // sky group: done by sky_kernel
+            (qi >= 0 && P.hist && flag(P.hf_prev)))
             continue;
         const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
-        exp_pad<4>();                                          // experiment: per group
         const int ln = lane_id_fresh();
         const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
         const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
@@ -1634,8 +1281,6 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const int py = P.row0 + pr * P.row_step;
         const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
         const bool me = valid && sub_g == 0 && px == P.dbg_x && py == P.dbg_y;
-        const int skyflag = (RT_EXP_SKYCMP && P.gsky) ? (int)flag(P.gsky) : -1;
-        int skybad = 0;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
@@ -1647,21 +1292,16 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
             if (act) {
                 const float2 o = spp_offset_dev(k);
-#if RT_EXP_NOCAM                                               // experiment: no camera ray
-                r0.d = v3((float)px + o.x, (float)py + o.y, 1.0f);
-#else
                 DCamera cam = kld(P.cam);
                 cam.W = fresh_s(cam.W); cam.H = fresh_s(cam.H); cam.near_ = fresh_s(cam.near_);
                 r0 = camera_at(cam, (float)px + o.x, (float)py + o.y);
-#endif
             }
             if (rd == 0 && last_of_batch) request(qi);         // next ticket, in flight during the trace
             // Whole-group miss (fast kernels): when no lane's primary ray hits a child of the
             // tree's root -- the traversal's first step, same test -- every sample misses, its
             // radiance is the integrator's initial zero (scene.cu:124-126) and the group's
             // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
-            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && (RT_EXP_SKYCMP || !RT_SKY_PERRAY || !kparams().gsky) && !__ballot(ft_root_hit(S, bv, act, r0))) {
-                if (skyflag == 0) skybad = 1;
+            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && !kparams().gsky && !__ballot(ft_root_hit(S, bv, act, r0))) {
                 if (act && k == 0) {
                     int op = pix_index;
                     opaque(op);
@@ -1670,14 +1310,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                 }
                 break;                                         // sum_c = sum_r = 0
             }
-            if (skyflag == 1) skybad = 2;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
-#if RT_EXP_NOTRACE                                             // experiment: group overhead only
-            V4 c = v4(r0.d.x, r0.d.y, r0.d.z, 1.0f);
-#else
             V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
-#endif
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
                 return v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y, v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);
@@ -1694,9 +1329,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             int bb = base_g;
             opaque(bb);
             const V4 cc = clamp1(c);
-            if (RT_EXP_NORED) {                                // experiment: no sample reduction
-                sum_c = sum_c + c;
-            } else if (L == 8) {                               // spp = 8: all permutes in one LDS round trip
+            if (L == 8) {                               // spp = 8: all permutes in one LDS round trip
                 V4 v[8];
 #pragma unroll
                 for (int s = 0; s < 8; s++) v[s] = shfl4(cc, bb + s);
@@ -1736,14 +1369,14 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
             const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
                                  ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
-            if (P.rgba) P.rgba[p] = (RT_EXP_SKYCMP && skybad) ? 0xDEAD0000u + (unsigned)skybad : enc;
+            if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(mean(sum_r.x), mean(sum_r.y), mean(sum_r.z), mean(sum_r.w));
         }
         if (STATS && P.stats && lane == 0) {                 // profiling: heaviest group (PROF: rt_profile_groups)
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
-        if (!RT_EXP_NOREC && kparams().hist) {                 // record for the next frame's order
+        if (kparams().hist) {                 // record for the next frame's order
             KTP& P = kparams();
             const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;   // wave-uniform (scalar)
             const bool heavy = dur > thr;
@@ -1886,15 +1519,15 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     if (wv == 0) {
         const int gl = base + lane;
         const bool in = lane < n_in;
-        const bool csky = in && RT_SKY_CONE && cone_misses_root(P, S, gl);
-        // Representative ray (RT_SKY_REP): a group the cone test leaves undecided is live as
+        const bool csky = in && cone_misses_root(P, S, gl);
+        // Representative ray: a group the cone test leaves undecided is live as
         // soon as one of its primaries enters the root -- lane 0's (pixel 0, sample 0), the
         // trace kernel's own ray and test -- so only the groups whose representative misses
         // need the 64-ray test below.  One group per lane here.
         bool rlive = false;
-        if (RT_SKY_REP && !RT_EXP_SKYCMP && in && !csky) {
+        if (in && !csky) {
             const int gy = (int)udiv((unsigned)gl, P.div_ngx), gx = gl - gy * P.n_gx;
-            const float2 o = P.spp_off[0];
+            const float2 o = spp_offset_dev(0);
             const Ray rr = camera_at(P.cam, (float)(gx * P.gw) + o.x, (float)(P.row0 + gy * P.gh * P.row_step) + o.y);
             BvhRefs bv{};
             bv.fnode = S.fnode;
@@ -1930,7 +1563,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
         if (P.radiance) P.radiance[pix_index] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     };
     const unsigned long long skym = s_sky;
-    if (!RT_EXP_SKYCMP && skym)
+    if (skym)
         for (int i = threadIdx.x; i < 64 * P.px_per_wave; i += SKY_THREADS) {
             const int gi = i / P.px_per_wave;
             if ((skym >> gi) & 1) sky_pixel(base + gi, i - gi * P.px_per_wave);
@@ -1941,11 +1574,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
     const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
     const bool lane_ok = pix_g < P.px_per_wave && sub_g < P.spp;   // k = sub_g (spp <= 64: one round)
-    unsigned long long todo = RT_SKY_PERRAY ? s_todo : 0ull;
-    if (!RT_SKY_PERRAY && threadIdx.x < 64 && ((s_todo >> threadIdx.x) & 1)) {   // undecided: live, the trace kernel tests them
-        gsky[base + threadIdx.x] = 0;
-        s_list[atomicAdd(&s_cnt, 1)] = base + threadIdx.x;
-    }
+    unsigned long long todo = s_todo;
     for (int k = 0; todo; k++) {
         const int bit = __builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1958,7 +1587,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
         const bool act = valid && lane_ok;
         Ray r0{v3(0, 0, 0), v3(0, 0, 1)};
         if (act) {
-            const float2 o = P.spp_off[sub_g];                 // the host table (same values as spp_offset_dev)
+            const float2 o = spp_offset_dev(sub_g);            // the trace kernel's own offsets
             r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
         }
         BvhRefs bv{};
@@ -1969,7 +1598,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
             if (sky && P.hist) P.hf_next[g] = 0;
             if (!sky) s_list[atomicAdd(&s_cnt, 1)] = g;
         }
-        if (sky && !RT_EXP_SKYCMP && valid && sub_g == 0) sky_pixel(g, pix_g);
+        if (sky && valid && sub_g == 0) sky_pixel(g, pix_g);
     }
     __syncthreads();
     const int q = blockIdx.x % NQ, n = s_cnt;
@@ -1979,43 +1608,6 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     if (threadIdx.x < n) live[q * P.live_cap + s_base + threadIdx.x] = s_list[threadIdx.x];
 }
 
-// Experiment kernel (profiling aid, not on the product path): closest hit of the
-// primary rays only, persistent blocks with the BVH in LDS, one sample per lane.
-template <bool LDS, bool NOLEAF, int WORK>
-__global__ __launch_bounds__(TRACE_BLOCK_P) void primary_only_kernel(TraceParams P, SceneView S, float4* out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const BvhRefs bv = stage_bvh<LDS>(S, smem);
-    const int lane = threadIdx.x & 63;
-    const int L = P.lanes_per_px;
-    const int pix = lane / L, sub = lane - pix * L;
-    WaveCounters wc{0, 0, 0, 0};
-    const int wave_id = blockIdx.x * (TRACE_BLOCK_P / 64) + (threadIdx.x >> 6);
-    const int n_waves = gridDim.x * (TRACE_BLOCK_P / 64);
-    int g = WORK == 0 ? 0 : wave_id - n_waves;
-    for (;;) {
-        if (WORK == 0) {                     // one atomic per group
-            int t = 0;
-            if (lane == 0) t = atomicAdd(P.work, 1);
-            g = __shfl(t, 0);
-        } else {                             // static stride
-            g += n_waves;
-        }
-        if (g >= P.n_groups) break;
-        const int gx = g % P.n_gx, gy = g / P.n_gx;
-        const int px = gx * P.gw + pix % P.gw, pr = gy * P.gh + pix / P.gw;
-        const bool valid = pix < P.px_per_wave && px < P.W && pr < P.n_rows && sub < P.spp;
-        const int py = P.row0 + pr * P.row_step;
-        Ray r{v3(0, 0, 0), v3(0, 0, 1)};
-        if (valid) { float2 o = P.spp_off[sub]; r = camera_at(P.cam, (float)px + o.x, (float)py + o.y); }
-        Best b; b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0; b.v = 0;
-        bool h = closest_hit<NOLEAF, true>(S, bv, valid, r, b, wc);
-        if (valid) out[((size_t)pr * P.W + px) * P.lanes_per_px + sub] = make_float4(h ? b.time : -1.0f, __int_as_float(b.inst), b.u, b.v);
-    }
-    if (P.stats && lane == 0) {
-        atomicAdd(&P.stats[0], wc.rays); atomicAdd(&P.stats[1], wc.nodes);
-        atomicAdd(&P.stats[2], wc.leaves); atomicAdd(&P.stats[3], wc.tris);
-    }
-}
 // ---------------------------------------------------------------------------
 // BVH build: ropt::gpu::BVH::BVH (bvh.cu:74-91) + create_boxes (raytracer.cu:54-74)
 // in one workgroup.  Output: heap-ordered nodes[1 .. 2n-1].
@@ -2094,12 +1686,6 @@ __host__ __device__ inline void fnode_split(const unsigned long long* k, int nr,
     last = i < j ? j : i;
 }
 
-#ifdef RT_BUILD_STAMPS      // experiment builds only: phase timestamps of the BVH build
-__device__ unsigned long long g_build_stamps[16];
-#define BSTAMP(i) do { __syncthreads(); if (threadIdx.x == 0) g_build_stamps[i] = wall_clock64(); } while (0)
-#else
-#define BSTAMP(i) do {} while (0)
-#endif
 template <bool LDS_TREE>
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2110,7 +1696,6 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     else tree.t = A.tree;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n = A.n;
-    BSTAMP(0);
     for (int i = tid; i < A.n_work; i += nt) A.work[i] = 0;
     if (A.hctl && tid < 2) A.hctl[tid] = 0;
 
@@ -2127,7 +1712,6 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         idx[i] = i;
     }
     __syncthreads();
-    BSTAMP(1);
     // Sort on (key, index): identical order to a stable sort by key (thrust sort_by_key,
     // bvh.cu:86).  Entries [n_inst, n) are padding with key ~0 and the largest indices, so
     // they already sit at their rank; only [0, n_inst) moves.
@@ -2226,12 +1810,10 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             __syncthreads();
         }
     }
-    BSTAMP(2);
     // reorder (bvh.cu:34-41: the box is recomputed, same arithmetic) and pairwise level
     // merges (bvh.cu:43-61)
     for (int i = tid; i < n; i += nt) tree.put(i, inst_box(idx[i]));
     __syncthreads();
-    BSTAMP(3);
     {
         int lvl = 0, size = n, out = n;
         while (size >= 2) {
@@ -2240,7 +1822,6 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             lvl += size; out += size / 2; size >>= 1;
         }
     }
-    BSTAMP(4);
     // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
     for (int k = tid; k < 2 * n; k += nt) {
         Box b;
@@ -2255,7 +1836,6 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     // leaves.  Internal node i splits at the highest differing key bit; the child
     // whose leaves are later in storage order is child A (visited first), so
     // leaves are met in the heap's DFS order (heap leaf k <-> storage 2n-1-k).
-    BSTAMP(5);
     const int nr = A.n_real;                    // real leaves = storage [0, nr) (padding sorts last)
     for (int i = tid; i < nr - 1; i += nt) {
         int first, last, gamma;
@@ -2278,67 +1858,6 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
         }
         refs[2] = refs[3] = 0;
     }
-    BSTAMP(6);
-#if RT_QUAD
-    // 4-wide records of the fast kernel (QNode, after the binary records): binary node i at
-    // even depth (the root at 0) becomes quad node qid[i], whose four slots are its children's
-    // children in DFS order -- child A's two children (or A itself when A is a leaf, then an
-    // empty slot), then B's.  The internal slots are binary nodes at even depth again.  The set
-    // of leaves a ray hits and their order are those of the binary tree (a hit leaf's ancestors
-    // are hit: the slab test is monotone in the box), the skipped odd-depth boxes only cull.
-    // Layout per quad node: 7 float4 = pair (slot 0, 1) and pair (slot 2, 3) in the binary
-    // record's interleaved form, then the four refs (node index >= 0, -1 - instance for a leaf,
-    // QEMPTY).  The LDS of the phases above is reused: par | qid | 16 wave partials.
-    __syncthreads();
-    if (nr >= 2) {
-        const int m = nr - 1;                                  // binary internal nodes
-        int* par = reinterpret_cast<int*>(smem);
-        int* qid = par + m;
-        int* wsum = qid + m;
-        auto bref = [&](int i, int c) { return reinterpret_cast<const int*>(A.fnode + 4 * (size_t)i + 3)[c]; };
-        for (int i = tid; i < m; i += nt) par[i] = -1;
-        __syncthreads();
-        for (int i = tid; i < m; i += nt)
-            for (int c = 0; c < 2; c++) { const int ch = bref(i, c); if (ch >= 0) par[ch] = i; }
-        __syncthreads();
-        const int chunk = (m + nt - 1) / nt, b0 = min(m, tid * chunk), b1 = min(m, b0 + chunk);
-        int cnt = 0;
-        for (int i = b0; i < b1; i++) {
-            int d = 0;
-            for (int p = par[i]; p >= 0 && d < 64; p = par[p]) d++;
-            qid[i] = (d & 1) ? -1 : 0;
-            cnt += (d & 1) ? 0 : 1;
-        }
-        const int ln = tid & 63, wv = tid >> 6;
-        int inc = cnt;                                         // inclusive scan over the wave
-        for (int o = 1; o < 64; o <<= 1) { const int v = __shfl_up(inc, o); if (ln >= o) inc += v; }
-        if (ln == 63) wsum[wv] = inc;
-        __syncthreads();
-        int base = inc - cnt;
-        for (int w = 0; w < wv; w++) base += wsum[w];
-        for (int i = b0; i < b1; i++) if (qid[i] == 0) qid[i] = base++;
-        __syncthreads();
-        float4* qn = A.fnode + 4 * (size_t)m;
-        for (int i = tid; i < m; i += nt) {
-            if (qid[i] < 0) continue;
-            float* q = reinterpret_cast<float*>(qn + 7 * (size_t)qid[i]);
-            int* qr = reinterpret_cast<int*>(qn + 7 * (size_t)qid[i] + 6);
-            const float* bi = reinterpret_cast<const float*>(A.fnode + 4 * (size_t)i);
-            for (int c = 0; c < 2; c++) {                      // child A -> slots 0, 1; B -> 2, 3
-                const int ch = bref(i, c);
-                float* qp = q + 12 * c;
-                for (int s = 0; s < 2; s++) {
-                    const float* src;                          // binary record and side of the slot's box
-                    int side, ref;
-                    if (ch >= 0) { src = reinterpret_cast<const float*>(A.fnode + 4 * (size_t)ch); side = s; ref = bref(ch, s); }
-                    else { src = bi; side = c; ref = s == 0 ? ch : QEMPTY; }   // a leaf child: itself, then empty
-                    for (int k = 0; k < 6; k++) qp[2 * k + s] = src[2 * k + side];
-                    qr[2 * c + s] = ref >= 0 ? qid[ref] : ref;
-                }
-            }
-        }
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2448,7 +1967,7 @@ struct rt_scene {
     DTri* d_tris = nullptr; DMesh* d_meshes = nullptr; DInst* d_insts = nullptr; DMat* d_mats = nullptr;
     DLight* d_lights = nullptr; Box* d_mesh_box = nullptr; Box* d_tree = nullptr;
     float4* d_node_pair = nullptr; int* d_leaf = nullptr;
-    float4* d_fnode = nullptr; int n_real = 0, fdepth = 0, n_quad = 0;   // ordered LBVH (fast kernel) + quad records
+    float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
     float4* d_inst4 = nullptr;
     TriAx* d_tri_ax = nullptr;                   // axis-plane triangle records (tri_axis_records)
     int* d_work = nullptr; int n_cu = 0;
@@ -2638,11 +2157,9 @@ std::vector<Box> mesh_boxes(const rt::Scene& h) {
     }
     return mbox;
 }
-// n_real, the deepest internal node's depth (root = 1) and the number of quad records
-// (RT_QUAD: internal nodes at odd depth here, i.e. even from a root at 0).
-void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth, int* n_quad) {
+// n_real and the deepest internal node's depth (root = 1).
+void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth) {
     const std::vector<Box> mbox = mesh_boxes(h);
-    *n_quad = 0;
     std::vector<std::pair<unsigned long long, int>> kv;
     bool ordered = true;                                      // every real box finite with mn <= mx
     for (size_t i = 0; i < h.d_insts.size(); i++) {
@@ -2677,7 +2194,6 @@ void ordered_tree_shape(const rt::Scene& h, int* n_real, int* depth, int* n_quad
         const auto [node, d] = todo.back();
         todo.pop_back();
         *depth = std::max(*depth, d);
-        *n_quad += d & 1;
         if (d > nr) { *depth = 1 << 20; return; }          // malformed: disable the fast tree
         for (int c = 0; c < 2; c++) if (child[2 * node + c] >= 0) todo.push_back({child[2 * node + c], d + 1});
     }
@@ -2721,9 +2237,9 @@ int upload(rt_scene* s) {
     s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
     HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
-    ordered_tree_shape(h, &s->n_real, &s->fdepth, &s->n_quad);
+    ordered_tree_shape(h, &s->n_real, &s->fdepth);
     s->shape_gen = s->inst_gen;
-    HIPCHK(hipMalloc((void**)&s->d_fnode, (RT_QUAD ? 11 : 4) * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));   // binary (+ quad)
+    HIPCHK(hipMalloc((void**)&s->d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_leaf, nl * sizeof(int)));
     HIPCHK(hipMalloc((void**)&s->d_inst4, std::max<size_t>(1, h.d_insts.size()) * sizeof(float4)));
     HIPCHK(hipMalloc((void**)&s->d_work, WORK_INTS * sizeof(int)));
@@ -2787,7 +2303,7 @@ int sync_slot_insts(rt_scene* s, hipStream_t st) {
 void refresh_shape(rt_scene* s) {
     if (s->shape_gen == s->inst_gen) return;
     int nr = 0;
-    ordered_tree_shape(s->h, &nr, &s->fdepth, &s->n_quad);
+    ordered_tree_shape(s->h, &nr, &s->fdepth);
     s->shape_gen = s->inst_gen;
 }
 
@@ -2813,7 +2329,7 @@ int ensure_other_slot(rt_scene* s) {
         rt_scene::Slot& o = s->store[i];
         if (i == s->cur_slot || o.d_work) continue;
         HIPCHK(hipMalloc((void**)&o.d_node_pair, 3 * nl * sizeof(float4)));
-        HIPCHK(hipMalloc((void**)&o.d_fnode, (RT_QUAD ? 11 : 4) * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));   // binary (+ quad)
+        HIPCHK(hipMalloc((void**)&o.d_fnode, 4 * (size_t)std::max(1, s->n_real - 1) * sizeof(float4)));
         HIPCHK(hipMalloc((void**)&o.d_leaf, nl * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_tree, 2 * nl * sizeof(Box)));
         HIPCHK(hipMalloc((void**)&o.d_work, WORK_INTS * sizeof(int)));
@@ -2862,7 +2378,7 @@ int ensure_history(rt_scene* s, int n_groups, const long long* key, hipStream_t 
     if (n_groups > s->hist_cap) {
         for (int p = 0; p < 2; p++) { dfree(s->d_hlist[p]); dfree(s->d_hflag[p]); }
         dfree(s->d_hctl);
-        const int cap = std::max(n_groups, 1024);
+        const int cap = (std::max(n_groups, 1024) + 3) & ~3;   // whole dwords (flag() reads scalar dwords)
         for (int p = 0; p < 2; p++) {
             HIPCHK(hipMalloc((void**)&s->d_hlist[p], cap * sizeof(int)));
             HIPCHK(hipMalloc((void**)&s->d_hflag[p], cap));
@@ -2926,11 +2442,8 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     SceneView v;
     v.tris = s->d_tris; v.meshes = s->d_meshes; v.insts = s->d_insts; v.mats = s->d_mats; v.lights = s->d_lights;
     v.node_pair = s->d_node_pair; v.leaf_inst = s->d_leaf;
-    v.fnode = s->d_fnode; v.n_real = s->n_real; v.n_quad = s->n_quad;
-#ifndef RT_NO_FTREE
-#define RT_NO_FTREE 0        // 1: profiling variant, the fast kernel walks the reference heap
-#endif
-    v.ftree = (!RT_NO_FTREE && s->n_real >= 2 && s->fdepth <= FT_MAX_DEPTH) ? 1 : 0; v.inst4 = s->d_inst4;
+    v.fnode = s->d_fnode; v.n_real = s->n_real;
+    v.ftree = (s->n_real >= 2 && s->fdepth <= FT_MAX_DEPTH) ? 1 : 0; v.inst4 = s->d_inst4;
     v.n_leaf = s->n_leaf; v.n_inst = (int)s->h.d_insts.size();
     v.n_lights = (int)s->h.d_lights.size(); v.use_bvh = use_bvh ? 1 : 0;
     v.n_mats = (int)s->h.d_mats.size(); v.n_tris = (int)s->h.d_tris.size(); v.n_meshes = (int)s->h.d_meshes.size();
@@ -2949,10 +2462,7 @@ SceneView view_of(const rt_scene* s, bool use_bvh) {
     const float radius = pmax + vmax + amax(s->h.d_cam.pos) + 1.0f;
     prune_ok = prune_ok && std::isfinite(radius);
     v.prune_abs = prune_ok ? 4e-4f * vmax + 0x1p-14f * radius : -1.0f;
-#ifndef RT_NO_AXIS
-#define RT_NO_AXIS 0         // 1: A/B variant without the axis-plane triangle path
-#endif
-    v.tri_ax = (!RT_NO_AXIS && v.ident_all && !s->h.d_tris.empty()) ? s->d_tri_ax : nullptr;
+    v.tri_ax = (v.ident_all && !s->h.d_tris.empty()) ? s->d_tri_ax : nullptr;
     return v;
 }
 
@@ -2996,9 +2506,6 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // in flight: 8-way slice 0.234 -> 0.229 ms; whole frames and 2-way slices keep 4 x 2
     // (8 x 1 there: +3.4% / +2%; profiles/r01/ab_group_shape_v31.log).
     if (o.row_step >= 8) gw = P.px_per_wave;
-#ifdef RT_GROUP_W                                          // experiment builds: fixed group width
-    if (P.px_per_wave % RT_GROUP_W == 0) gw = RT_GROUP_W;
-#endif
     P.gw = gw; P.gh = P.px_per_wave / gw;
     auto log2_exact = [](int v) { int k = 0; while ((1 << k) < v) k++; return (1 << k) == v ? k : -1; };
     P.l_shift = log2_exact(P.lanes_per_px); P.gw_shift = log2_exact(P.gw);
@@ -3011,7 +2518,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
     P.work = s->d_work; P.tpc = TPC;
     {   // unlit skip (trace_sample, ST_LIGHT): every incoming light must be >= +0 and finite
-        bool ok = RT_UNLIT_SKIP && !want_stats && !dbg && !prof;
+        bool ok = !want_stats && !dbg && !prof;
         auto pos0 = [](float v) { return std::isfinite(v) && !std::signbit(v); };
         for (const DLight& l : h.d_lights) ok = ok && pos0(l.col.x) && pos0(l.col.y) && pos0(l.col.z) && pos0(l.col.w);
         for (const DMat& m : h.d_mats)
@@ -3043,7 +2550,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
-    const bool shade = RT_SHADE_LDS && park && ft && S.tri_ax && !prof &&
+    const bool shade = park && ft && S.tri_ax && !prof &&
                        lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
     if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
         constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
@@ -3089,7 +2596,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // 4-way 0.360 / 0.360, 8-way 0.179-0.186 / 0.200-0.204; profiles/r02/hist_policy.log).
     P.hist = 0;
     const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
-    if (!want_stats && !dbg && !RT_EXP_NOHIST && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
+    if (!want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
         const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
         int r;
         if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
@@ -3104,7 +2611,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     s->work_zeroed = false;                                   // this launch consumes the counters
     s->hctl_zeroed = -1;
     // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
-    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0 && RT_SKY_PREPASS;
+    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
     if (sky) {
         if (P.n_groups > s->gsky_cap) {
             dfree(s->d_gsky);
@@ -3120,8 +2627,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
             s->live_cap = lcap * NQ;
         }
         P.gsky = s->d_gsky;
-        P.live = RT_EXP_SKYCMP ? nullptr : s->d_live; P.live_cap = lcap;
-        if (P.live) P.tpc = RT_TPC_LIVE;
+        P.live = s->d_live; P.live_cap = lcap;
+        P.tpc = RT_TPC_LIVE;
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
         HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
     }
@@ -3545,13 +3052,6 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     return RT_OK;
 }
 
-#ifdef RT_BUILD_STAMPS
-int rt_exp_build_stamps(unsigned long long* out) {
-    HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_build_stamps), 16 * sizeof(unsigned long long)));
-    return RT_OK;
-}
-#endif
 
 int rt_scene_set_frame_slots(rt_scene* s, int n) {
     CHECK_FINISHED(s);
@@ -3636,10 +3136,10 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap) {   // rayt
     return RT_OK;
 }
 
-// Profiling aid (not part of rt_amd.h's stable surface): run experiment `which`
-// (0/3 = primary-ray closest-hit only (atomic / static work), 1/2 = same without leaf
-// work, 4 = full trace with the occlusion early exit AND counters: the work actually
-// done) `reps` times; returns mean kernel ms and counters.
+// Profiling aid (not part of rt_amd.h's stable surface): run experiment `which` `reps`
+// times -- 4: the counted kernel with the occlusion early exit, 5: the counted kernel,
+// 6: the fast kernel's PROF variant (wave step counts, cycle split, and the queries the
+// fast kernel issues) -- and return the mean kernel ms and the counters.
 int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_t* counters) {
     CHECK_FINISHED(s);
     int r;
@@ -3672,52 +3172,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
         return RT_OK;
     }
-    if ((r = upload(s)) != RT_OK) return r;
-    HIPCHK(hipSetDevice(s->device));
-    if ((r = ensure_spp(s, spp)) != RT_OK) return r;
-    if ((r = begin_frame(s, sstream(s), true)) != RT_OK) return r;
-    if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
-    s->work_zeroed = false;                                  // the primary kernels reset d_work themselves
-    rt_render_opts o; rt_render_opts_default(&o); o.spp = spp;
-    TraceParams P{};
-    const rt::Scene& h = s->h;
-    P.cam = h.d_cam; P.W = h.cam.W; P.H = h.cam.H; P.row0 = 0; P.row_step = 1; P.n_rows = P.H; P.spp = spp;
-    P.spp_off = s->d_spp; P.stats = s->d_stats; P.work = s->d_work;
-    P.lanes_per_px = std::min(spp, 64); P.px_per_wave = 64 / P.lanes_per_px;
-    int gw = 1; while (gw * gw < P.px_per_wave) gw <<= 1;
-    P.gw = gw; P.gh = P.px_per_wave / gw; P.n_gx = (P.W + P.gw - 1) / P.gw;
-    P.n_groups = P.n_gx * ((P.n_rows + P.gh - 1) / P.gh);
-    SceneView S = view_of(s, true);
-    size_t lds = lds_bytes(S);
-    const void* fn = which == 1 ? (const void*)primary_only_kernel<true, true, 0>
-                   : which == 2 ? (const void*)primary_only_kernel<true, true, 1>
-                   : which == 3 ? (const void*)primary_only_kernel<true, false, 1>
-                                : (const void*)primary_only_kernel<true, false, 0>;
-    if (lds > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    int blocks = s->n_cu * per_cu;
-    float4* out = nullptr;
-    HIPCHK(hipMalloc((void**)&out, (size_t)P.W * P.H * P.lanes_per_px * sizeof(float4)));
-    float total = 0;
-    for (int i = 0; i < reps; i++) {
-        HIPCHK(hipMemsetAsync(s->d_work, 0, sizeof(int), sstream(s)));
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), sstream(s)));
-        HIPCHK(hipEventRecord(s->ev[0], sstream(s)));
-        void* args[] = {&P, &S, &out};
-        HIPCHK(hipLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, lds, sstream(s)));
-        HIPCHK(hipEventRecord(s->ev[1], sstream(s)));
-        HIPCHK(hipEventSynchronize(s->ev[1]));
-        float t = 0; HIPCHK(hipEventElapsedTime(&t, s->ev[0], s->ev[1]));
-        if (i > 0 || reps == 1) total += t;
-    }
-    if ((r = end_frame(s, sstream(s))) != RT_OK) return r;
-    unsigned long long v[22];
-    HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
-    if (counters) for (int i = 0; i < 22; i++) counters[i] = v[i];
-    if (ms) *ms = total / (reps > 1 ? reps - 1 : 1);
-    (void)hipFree(out);
-    return RT_OK;
+    return fail(RT_ERR_ARG, "experiment: 4 (counted, occlusion exit), 5 (counted), 6 (fast kernel, PROF counters)");
 }
 
 // Profiling aid (tools/group_profile.py, not on the product path): per-group durations
