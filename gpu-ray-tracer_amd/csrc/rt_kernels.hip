@@ -2850,7 +2850,10 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
     switch (what) {
         case RT_EXPORT_VERTICES: for (auto& v : h.verts) { f.push_back(v.x); f.push_back(v.y); f.push_back(v.z); } break;
         case RT_EXPORT_NORMALS: f = h.verts_norm; break;
-        case RT_EXPORT_TRIS: for (auto& t : h.tris) { iv.push_back(t.i0); iv.push_back(t.i1); iv.push_back(t.i2); iv.push_back(t.mat); } break;
+        case RT_EXPORT_TRIS:                                   // flattened (mesh) order: hit_tri indexes it
+            for (auto& m : h.meshes)
+                for (int i : m.tris) { const auto& t = h.tris[i]; iv.insert(iv.end(), {t.i0, t.i1, t.i2, t.mat}); }
+            break;
         case RT_EXPORT_MATERIALS:
             for (auto& m : h.mats) {
                 for (const V4* v : {&m.Ke, &m.Ka, &m.Kd, &m.Ks, &m.Kt, &m.Kr}) { f.push_back(v->x); f.push_back(v->y); f.push_back(v->z); f.push_back(v->w); }
@@ -2874,7 +2877,11 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
             f = {h.dist_atten.x, h.dist_atten.y, h.dist_atten.z, h.ambience.x, h.ambience.y, h.ambience.z, h.ambience.w};
             break;
         case RT_EXPORT_TEXCOORDS:
-            for (auto& t : h.tris) f.insert(f.end(), {(float)t.tex.has, t.tex.tx, t.tex.ty, t.tex.ux, t.tex.uy, t.tex.vx, t.tex.vy});
+            for (auto& m : h.meshes)
+                for (int i : m.tris) {
+                    const auto& t = h.tris[i];
+                    f.insert(f.end(), {(float)t.tex.has, t.tex.tx, t.tex.ty, t.tex.ux, t.tex.uy, t.tex.vx, t.tex.vy});
+                }
             break;
         case RT_EXPORT_ATLAS: {
             const size_t n = h.atlas_rgba.size();

@@ -86,7 +86,9 @@ int rt_scene_atlas_info(const rt_scene* s, int32_t atlas3[3]);
 
 /* info10 = {W, H, n_vertices, n_tris, n_meshes, n_instances, n_lights, n_point_lights, depth, n_materials} */
 int rt_scene_info(const rt_scene* s, int32_t info10[10]);
-/* Host copies of the scene arrays (layouts as in oracle/rt_oracle.h) for parity checks. */
+/* Host copies of the scene arrays (layouts as in oracle/rt_oracle.h) for parity checks.
+ * Triangles (and their texture coordinates) are listed in the flattened mesh order, the
+ * index space of rt_render_opts.hit_tri. */
 enum { RT_EXPORT_VERTICES = 0, RT_EXPORT_NORMALS = 1, RT_EXPORT_TRIS = 2, RT_EXPORT_MATERIALS = 3,
        RT_EXPORT_INSTANCES = 4, RT_EXPORT_INST_MESH = 5, RT_EXPORT_LIGHTS = 6, RT_EXPORT_CAMERA = 7, RT_EXPORT_ENV = 8,
        RT_EXPORT_TEXCOORDS = 9,   /* per triangle float7 {has, tx, ty, ux, uy, vx, vy} */

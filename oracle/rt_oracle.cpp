@@ -286,6 +286,11 @@ struct orc_scene {
     std::vector<uint8_t> atlas;      // textured mode (build extension): RGBA8 atlas
     int atlas_w = 0, atlas_h = 0;
     int textures = 0;
+    // SceneBuilder state (scene_builder.h:29-117) until orc_builder_finish flattens it:
+    // triangles per MeshBuilder, lights by kind (build_gpu_scene puts point lights first)
+    bool building = false;
+    std::vector<std::vector<Tri>> mesh_tris;
+    std::vector<Light> b_points, b_dirs;
 };
 
 namespace {
@@ -390,6 +395,7 @@ void build_cube(orc_scene& s, float scale, const Material& mat, const float* til
     V3 G = mul(scale, v3(-0.5f, -0.5f, 0.5f)), Hh = mul(scale, v3(0.5f, -0.5f, 0.5f));
     int mi = (int)s.mats.size(); s.mats.push_back(mat);
     Mesh m; m.e = Entity{Quat{0, 0, 0, 1}, v3(0, 0, 0)}; m.begin = (int)s.tris.size(); m.count = 0;
+    if (s.building) s.mesh_tris.emplace_back();
     const V3* faces[12][3] = {{&D, &A, &B}, {&C, &A, &D}, {&A, &E, &B}, {&E, &F, &B}, {&D, &B, &Hh}, {&B, &F, &Hh},
                               {&C, &G, &A}, {&A, &G, &E}, {&G, &Hh, &E}, {&E, &Hh, &F}, {&G, &C, &D}, {&D, &Hh, &G}};
     static const int axes[6][2] = {{0, 1}, {0, 2}, {2, 1}, {2, 1}, {0, 1}, {0, 2}};
@@ -409,8 +415,10 @@ void build_cube(orc_scene& s, float scale, const Material& mat, const float* til
             t.tex.ux = c[1][0] - c[0][0]; t.tex.uy = c[1][1] - c[0][1];
             t.tex.vx = c[2][0] - c[0][0]; t.tex.vy = c[2][1] - c[0][1];
         }
-        s.tris.push_back(t); m.count++;
+        if (s.building) s.mesh_tris.back().push_back(t);
+        else { s.tris.push_back(t); m.count++; }
     }
+    if (s.building) m.begin = m.count = 0;
     s.meshes.push_back(m);
 }
 
@@ -924,6 +932,114 @@ int orc_set_textures(orc_scene* s, int on) {
     return 0;
 }
 
+// ---- SceneBuilder (scene_builder.h:29-117, scene_builder.cc:11-29, scene_builder.cu:21-239) ----
+static Material mat26(const float* m) {                                      // material.h:14-31
+    Material r;
+    r.Ke = V4{m[0], m[1], m[2], m[3]}; r.Ka = V4{m[4], m[5], m[6], m[7]}; r.Kd = V4{m[8], m[9], m[10], m[11]};
+    r.Ks = V4{m[12], m[13], m[14], m[15]}; r.Kt = V4{m[16], m[17], m[18], m[19]}; r.Kr = V4{m[20], m[21], m[22], m[23]};
+    r.alpha = m[24]; r.eta = m[25];
+    return r;
+}
+int orc_scene_create(orc_scene** out) {
+    if (!out) return -1;
+    orc_scene* s = new orc_scene;
+    s->building = true;
+    *out = s;
+    return 0;
+}
+int orc_builder_add_vertex(orc_scene* s, float x, float y, float z) {       // SceneBuilder::add_vertex
+    if (!s || !s->building) return -1;
+    s->verts.push_back(v3(x, y, z));
+    return (int)s->verts.size() - 1;
+}
+int orc_builder_create_mesh(orc_scene* s, const float* pos, const float* q) {   // create_mesh(pos, rot)
+    if (!s || !s->building) return -1;
+    Mesh m;
+    m.e = Entity{q ? Quat{q[0], q[1], q[2], q[3]} : Quat{0, 0, 0, 1}, pos ? v3(pos[0], pos[1], pos[2]) : v3(0, 0, 0)};
+    m.begin = m.count = 0;
+    s->meshes.push_back(m);
+    s->mesh_tris.emplace_back();
+    return (int)s->meshes.size() - 1;
+}
+int orc_builder_add_triangle(orc_scene* s, int mesh, int i0, int i1, int i2, const float* m, const float* tex6) {
+    if (!s || !s->building || !m || mesh < 0 || mesh >= (int)s->meshes.size()) return -1;   // MeshBuilder::add_triangle
+    Tri t; t.i0 = i0; t.i1 = i1; t.i2 = i2;
+    t.mat = (int)s->mats.size(); s->mats.push_back(mat26(m));               // one Material per triangle
+    if (tex6) { t.tex.has = 1; t.tex.tx = tex6[0]; t.tex.ty = tex6[1]; t.tex.ux = tex6[2]; t.tex.uy = tex6[3]; t.tex.vx = tex6[4]; t.tex.vy = tex6[5]; }
+    s->mesh_tris[mesh].push_back(t);
+    return 0;
+}
+int orc_builder_add_trans(orc_scene* s, int mesh) {                          // add_trans: Transformation{hitable_idx}
+    if (!s || !s->building || mesh < 0 || mesh >= (int)s->meshes.size()) return -1;
+    s->insts.push_back(Inst{Entity{Quat{0, 0, 0, 1}, v3(0, 0, 0)}, mesh});
+    return (int)s->insts.size() - 1;
+}
+int orc_builder_build_cube(orc_scene* s, float scale, const float* m, const float* tile3) {
+    if (!s || !s->building || !m) return -1;
+    build_cube(*s, scale, mat26(m), tile3);
+    return (int)s->meshes.size() - 1;
+}
+int orc_builder_add_point_light(orc_scene* s, const float* pos, const float* col) {
+    if (!s || !s->building || !pos || !col) return -1;
+    s->b_points.push_back(Light{0, v3(pos[0], pos[1], pos[2]), V4{col[0], col[1], col[2], col[3]}});
+    return 0;
+}
+int orc_builder_add_directional_light(orc_scene* s, const float* dir, const float* col) {
+    if (!s || !s->building || !dir || !col) return -1;                      // DirLight::set_shine_dir normalizes
+    s->b_dirs.push_back(Light{1, normalized(v3(dir[0], dir[1], dir[2])), V4{col[0], col[1], col[2], col[3]}});
+    return 0;
+}
+// build_gpu_scene(Canvas, Camera) + Environment (scene_builder.cu:21-100, camera.cu:6-9,
+// environment.h:19-93): meshes flattened in creation order, normals generated, point lights
+// before directional ones.
+int orc_builder_finish(orc_scene* s, int W, int H, float fov, float unit, const float* cpos, const float* cq,
+                       const float* da, const float* amb, int depth) {
+    if (!s || !s->building || W <= 0 || H <= 0 || !(unit > 0) || depth < 0 || depth >= MAX_DEPTH) return -1;
+    for (size_t m = 0; m < s->meshes.size(); m++) {
+        s->meshes[m].begin = (int)s->tris.size();
+        s->meshes[m].count = (int)s->mesh_tris[m].size();
+        for (const Tri& t : s->mesh_tris[m]) {
+            if (t.i0 < 0 || t.i1 < 0 || t.i2 < 0 || t.i0 >= (int)s->verts.size() || t.i1 >= (int)s->verts.size() ||
+                t.i2 >= (int)s->verts.size()) return -1;
+            s->tris.push_back(t);
+        }
+    }
+    s->lights = s->b_points; s->n_point = (int)s->b_points.size();
+    s->lights.insert(s->lights.end(), s->b_dirs.begin(), s->b_dirs.end());
+    s->W = W; s->H = H;
+    s->cam.e = Entity{cq ? Quat{cq[0], cq[1], cq[2], cq[3]} : Quat{0, 0, 0, 1}, cpos ? v3(cpos[0], cpos[1], cpos[2]) : v3(0, 0, 0)};
+    s->cam.near_ = 0.5f * W / unit / tanf(fov);                              // camera.cu:7 (nvcc TU: tanf)
+    s->cam.unit = unit; s->cam.W = (float)W; s->cam.H = (float)H;
+    if (da) s->dist_atten = v3(da[0], da[1], da[2]);
+    if (amb) s->ambience = V4{amb[0], amb[1], amb[2], amb[3]};
+    s->depth = depth;
+    generate_normals(*s);
+    s->building = false;
+    s->mesh_tris.clear();
+    return 0;
+}
+// Entity::set_position / set_orientation of the camera (entity.h:49-74; Camera::at reads them,
+// camera.cu:33-42) and of instance i's Transformation (get_transformation(i), entity.cu:5-37).
+int orc_set_camera(orc_scene* s, const float* pos, const float* q) {
+    if (!s || s->building) return -1;
+    if (pos) s->cam.e.p = v3(pos[0], pos[1], pos[2]);
+    if (q) s->cam.e.o = Quat{q[0], q[1], q[2], q[3]};
+    return 0;
+}
+int orc_set_trans(orc_scene* s, int i, const float* pos, const float* q) {
+    if (!s || i < 0 || i >= (int)s->insts.size()) return -1;
+    if (pos) s->insts[i].e.p = v3(pos[0], pos[1], pos[2]);
+    if (q) s->insts[i].e.o = Quat{q[0], q[1], q[2], q[3]};
+    return 0;
+}
+int orc_set_env(orc_scene* s, const float* amb, const float* da, int depth) {   // Environment setters
+    if (!s || depth < 0 || depth >= MAX_DEPTH) return -1;
+    if (amb) s->ambience = V4{amb[0], amb[1], amb[2], amb[3]};
+    if (da) s->dist_atten = v3(da[0], da[1], da[2]);
+    s->depth = depth;
+    return 0;
+}
+
 int orc_scene_counts(const orc_scene* s, int32_t* c) {
     c[0] = s->W; c[1] = s->H; c[2] = (int)s->verts.size(); c[3] = (int)s->tris.size(); c[4] = (int)s->meshes.size();
     c[5] = (int)s->insts.size(); c[6] = (int)s->lights.size(); c[7] = s->n_point; c[8] = s->depth; c[9] = (int)s->mats.size();
@@ -976,6 +1092,7 @@ int orc_build_bvh(const orc_scene* s, float* boxes, int32_t* ordering, int max_n
 int orc_render(const orc_scene* s, int sem, int use_bvh, int spp, int row0, int row_step, int nthreads,
                uint32_t* rgba, float* rad, int32_t* hi, int32_t* ht, uint64_t* stats) {
     if (spp < 1 || row_step < 1 || row0 < 0) { g_err = "bad arguments"; return -1; }
+    if (s->building) { g_err = "builder scene not finished"; return -1; }
     BVH bvh = build_bvh(*s, sem == ORC_SEM_CPU);
     std::vector<int> rows;
     for (int y = row0; y < s->H; y += row_step) rows.push_back(y);

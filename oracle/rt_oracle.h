@@ -43,6 +43,25 @@ int orc_set_atlas(orc_scene* s, const uint8_t* rgba8, int width, int height);
 int orc_set_textures(orc_scene* s, int on);
 const char* orc_last_error(void);
 
+/* SceneBuilder (scene_builder.h:29-117): an empty scene, then the builder calls, then
+ * finish (build_gpu_scene with Canvas W x H and Camera(fov radians, unit), Environment).
+ * Index-returning calls return the new index (>= 0) or -1.  material26 as rt_amd.h. */
+int orc_scene_create(orc_scene** out);
+int orc_builder_add_vertex(orc_scene* s, float x, float y, float z);
+int orc_builder_create_mesh(orc_scene* s, const float* pos3, const float* quat4);
+int orc_builder_add_triangle(orc_scene* s, int mesh, int i0, int i1, int i2, const float* material26, const float* tex6);
+int orc_builder_add_trans(orc_scene* s, int mesh);
+int orc_builder_build_cube(orc_scene* s, float scale, const float* material26, const float* tile3);
+int orc_builder_add_point_light(orc_scene* s, const float* pos3, const float* col4);
+int orc_builder_add_directional_light(orc_scene* s, const float* dir3, const float* col4);
+int orc_builder_finish(orc_scene* s, int width, int height, float fov, float unit, const float* cam_pos3,
+                       const float* cam_quat4, const float* dist_atten3, const float* ambience4, int depth);
+/* Camera / instance poses (Entity::set_position / set_orientation, entity.h:49-74) and
+ * the Environment (ambience, distance attenuation, depth).  NULL leaves a field as is. */
+int orc_set_camera(orc_scene* s, const float* pos3, const float* quat4);
+int orc_set_trans(orc_scene* s, int trans, const float* pos3, const float* quat4);
+int orc_set_env(orc_scene* s, const float* ambience4, const float* dist_atten3, int depth);
+
 /* Scene introspection: counts = {W, H, n_vertices, n_tris, n_meshes, n_instances, n_lights, n_point, depth, n_mats} */
 int orc_scene_counts(const orc_scene* s, int32_t* counts10);
 /* float dumps of the scene exactly as the reference builds it */

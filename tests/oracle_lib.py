@@ -44,6 +44,19 @@ class Oracle:
         L.orc_spp_offset.argtypes = [ctypes.c_int, _f, _f]
         L.orc_set_atlas.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.orc_set_textures.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        vp, fl = ctypes.c_void_p, ctypes.c_float
+        L.orc_scene_create.argtypes = [ctypes.POINTER(vp)]
+        L.orc_builder_add_vertex.argtypes = [vp, fl, fl, fl]
+        L.orc_builder_create_mesh.argtypes = [vp, vp, vp]
+        L.orc_builder_add_triangle.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
+        L.orc_builder_add_trans.argtypes = [vp, ctypes.c_int]
+        L.orc_builder_build_cube.argtypes = [vp, fl, vp, vp]
+        L.orc_builder_add_point_light.argtypes = [vp, vp, vp]
+        L.orc_builder_add_directional_light.argtypes = [vp, vp, vp]
+        L.orc_builder_finish.argtypes = [vp, ctypes.c_int, ctypes.c_int, fl, fl, vp, vp, vp, vp, ctypes.c_int]
+        L.orc_set_camera.argtypes = [vp, vp, vp]
+        L.orc_set_trans.argtypes = [vp, ctypes.c_int, vp, vp]
+        L.orc_set_env.argtypes = [vp, vp, vp, ctypes.c_int]
         self.L = L
 
     # -- scenes ---------------------------------------------------------------
@@ -53,6 +66,12 @@ class Oracle:
         if r != 0:
             raise RuntimeError("oracle load failed: %s" % self.L.orc_last_error().decode())
         return OracleScene(self, s)
+
+    def create(self):
+        """Empty scene for the SceneBuilder calls (OracleScene.add_vertex ... finish)."""
+        s = ctypes.c_void_p()
+        assert self.L.orc_scene_create(ctypes.byref(s)) == 0
+        return OracleScene(self, s, building=True)
 
     def spp_offset(self, k):
         dx, dy = ctypes.c_float(), ctypes.c_float()
@@ -126,9 +145,27 @@ class Oracle:
         raise KeyError(op)
 
 
+def _fa(a, n):
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a, np.float32)
+    assert a.size == n, (a.size, n)
+    return a
+
+
+def _vp(a):
+    return None if a is None else a.ctypes.data
+
+
 class OracleScene:
-    def __init__(self, orc, h):
+    def __init__(self, orc, h, building=False):
         self.orc, self.h = orc, h
+        self.W = self.H = self.depth = 0
+        if not building:
+            self._counts()
+
+    def _counts(self):
+        orc, h = self.orc, self.h
         c = np.zeros(10, np.int32)
         orc.L.orc_scene_counts(h, c.ctypes.data)
         (self.W, self.H, self.n_vertices, self.n_tris, self.n_meshes, self.n_instances, self.n_lights,
@@ -141,6 +178,57 @@ class OracleScene:
 
     def set_textures(self, on=True):
         assert self.orc.L.orc_set_textures(self.h, int(on)) == 0
+
+    # -- SceneBuilder (scene_builder.h:29-117) ---------------------------------
+    def _idx(self, r):
+        assert r >= 0, r
+        return r
+
+    def add_vertex(self, x, y, z):
+        return self._idx(self.orc.L.orc_builder_add_vertex(self.h, x, y, z))
+
+    def create_mesh(self, pos=(0, 0, 0), quat=(0, 0, 0, 1)):
+        p, q = _fa(pos, 3), _fa(quat, 4)
+        return self._idx(self.orc.L.orc_builder_create_mesh(self.h, _vp(p), _vp(q)))
+
+    def add_triangle(self, mesh, i0, i1, i2, mat, tex6=None):
+        m, t = _fa(mat, 26), _fa(tex6, 6)
+        assert self.orc.L.orc_builder_add_triangle(self.h, mesh, i0, i1, i2, _vp(m), _vp(t)) == 0
+
+    def add_trans(self, mesh):
+        return self._idx(self.orc.L.orc_builder_add_trans(self.h, mesh))
+
+    def build_cube(self, scale, mat, tile=None):
+        m, t = _fa(mat, 26), _fa(tile, 3)
+        return self._idx(self.orc.L.orc_builder_build_cube(self.h, scale, _vp(m), _vp(t)))
+
+    def add_point_light(self, pos, col):
+        p, c = _fa(pos, 3), _fa(col, 4)
+        assert self.orc.L.orc_builder_add_point_light(self.h, _vp(p), _vp(c)) == 0
+
+    def add_directional_light(self, d, col):
+        p, c = _fa(d, 3), _fa(col, 4)
+        assert self.orc.L.orc_builder_add_directional_light(self.h, _vp(p), _vp(c)) == 0
+
+    def finish(self, width, height, fov, unit, cam_pos=(0, 0, 0), cam_quat=(0, 0, 0, 1), dist_atten=(0, 0, 0),
+               ambience=(0, 0, 0, 0), depth=0):
+        a = [_fa(cam_pos, 3), _fa(cam_quat, 4), _fa(dist_atten, 3), _fa(ambience, 4)]
+        assert self.orc.L.orc_builder_finish(self.h, width, height, fov, unit, *[_vp(x) for x in a], depth) == 0
+        self._counts()
+
+    # -- poses / environment (Entity setters, entity.h:49-74) -------------------
+    def set_camera(self, pos=None, quat=None):
+        p, q = _fa(pos, 3), _fa(quat, 4)
+        assert self.orc.L.orc_set_camera(self.h, _vp(p), _vp(q)) == 0
+
+    def set_trans(self, t, pos=None, quat=None):
+        p, q = _fa(pos, 3), _fa(quat, 4)
+        assert self.orc.L.orc_set_trans(self.h, t, _vp(p), _vp(q)) == 0
+
+    def set_env(self, ambience=None, dist_atten=None, depth=None):
+        a, d = _fa(ambience, 4), _fa(dist_atten, 3)
+        assert self.orc.L.orc_set_env(self.h, _vp(a), _vp(d), self.depth if depth is None else depth) == 0
+        self._counts()
 
     def __del__(self):
         try:

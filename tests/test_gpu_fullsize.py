@@ -1,0 +1,114 @@
+"""Parity at the sizes the bench and BASELINE.json's configs run, against the
+oracle (raytracer.cu:17-43 sample semantics: build-defined spp offsets, per-sample clamp,
+k-ordered sum, truncating RGBA8):
+
+- config 4 / the bench's headline: world8_stress 1920x1080 8 spp rendered exactly as bench.py
+  renders it -- four frame slots, frames on rotating streams (FramePipeline), fast kernels with
+  the sky pre-pass -- on one GPU, and as 2 / 8 row-cyclic rank slices reassembled;
+- config 3: world8 1920x1080 8 spp; config 2: world1 1920x1080 brute force (counters too);
+- config 5's sample mapping at a reduced size: world16 and world16_tex (textured mode) at
+  320x180 with spp = 64 (64 lanes per pixel, one pixel per wave, 1x1 sky cones, the generic
+  reduction) and spp = 96 (the M_MULTI rounds), fast and counted kernels.
+The oracle runs on up to 16 host threads (a few seconds per 1080p frame)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, scene_path
+from twin import NTHREADS, assert_frames_equal
+
+pytestmark = pytest.mark.gpu
+WANT = ("rgba", "radiance", "hit_inst", "hit_tri")
+W, H = 1920, 1080
+
+
+@pytest.fixture(scope="module")
+def stress_1080p(oracle):
+    return oracle.render(oracle.load(scene_path("world8_stress"), W, H), spp=8, nthreads=NTHREADS)
+
+
+def _pipelined(gpu, scene, spp, world=1, rank=0, depth=4, n_frames=7, textures=False):
+    """This rank's rows of the last of n_frames frames issued as bench.py issues them."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+    import rtamd.dist as rtdist
+    s = gpu.Scene.load_json(scene_path(scene), W, H)
+    s.set_frame_slots(depth)
+    pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", depth=depth)
+    for k in range(n_frames):
+        pipe.step(k, lambda buf, st: s.render_device(spp=spp, row0=rank, row_step=world, compact=True,
+                                                     rgba_ptr=buf.data_ptr(), stream=st.cuda_stream,
+                                                     textures=textures))
+    out = pipe.finish()
+    torch.cuda.synchronize()
+    return out[:len(range(rank, H, world))].cpu().numpy().view(np.uint32)
+
+
+def test_bench_frame_world8_stress_1080p(gpu, stress_1080p):
+    """The headline frame: pipelined fast frames (RGBA8 as the bench keeps it), then one fast
+    frame with every output, against the oracle."""
+    rgba = _pipelined(gpu, "world8_stress", 8)
+    assert_frames_equal({"rgba": rgba}, stress_1080p, keys=("rgba",), ctx="pipelined")
+    s = gpu.Scene.load_json(scene_path("world8_stress"), W, H)
+    fr = s.render(spp=8, want=WANT, stats=False)
+    assert np.array_equal(fr["rgba"], rgba)
+    assert_frames_equal(fr, stress_1080p, ctx="fast")
+    assert (fr["hit_inst"] >= 0).mean() > 0.1
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_rank_slices_world8_stress_1080p(gpu, stress_1080p, world):
+    """Every rank's slice (rows r, r+N, ...; compact; one-row pixel groups at N = 8) rendered
+    through its own four-deep pipeline, reassembled as rank 0's un-permute does."""
+    frame = np.zeros((H, W), np.uint32)
+    for r in range(world):
+        frame[r::world] = _pipelined(gpu, "world8_stress", 8, world=world, rank=r, n_frames=5)
+    assert_frames_equal({"rgba": frame}, stress_1080p, keys=("rgba",), ctx=world)
+
+
+def test_world8_1080p_8spp(gpu, oracle):
+    s = gpu.Scene.load_json(scene_path("world8"), W, H)
+    fr = s.render(spp=8, want=WANT, stats=False)
+    assert_frames_equal(fr, oracle.render(oracle.load(scene_path("world8"), W, H), spp=8, nthreads=NTHREADS))
+    assert np.array_equal(_pipelined(gpu, "world8", 8, n_frames=5), fr["rgba"])
+
+
+def test_world1_1080p_brute_force(gpu, oracle):
+    """Config 2 (reference -r): every ray tests both instances; counters equal the oracle's."""
+    s = gpu.Scene.load_json(scene_path("world1"), W, H)
+    of = oracle.render(oracle.load(scene_path("world1"), W, H), use_bvh=0, spp=1, nthreads=NTHREADS)
+    full = s.render(spp=1, use_bvh=False, want=WANT, stats=True)
+    assert_frames_equal(full, of, ctx="counted")
+    st = full["stats"]
+    assert (st["rays"], st["nodes"], st["leaves"], st["tri_tests"]) == tuple(int(x) for x in of["stats"])
+    assert st["rays"] == 2084662                               # SURVEY Appendix D (the reference's count)
+    fast = s.render(spp=1, use_bvh=False, want=WANT, stats=False)
+    for k in WANT:
+        assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
+
+
+@pytest.mark.parametrize("scene,textures", [("world16", False), ("world16_tex", True)])
+@pytest.mark.parametrize("spp", [64, 96])
+def test_config5_sample_mapping(gpu, oracle, scene, textures, spp):
+    """Config 5 (world16, 64 spp, textured) at 320x180: the 64-lanes-per-pixel mapping and the
+    multi-round (spp > 64) kernels, fast and counted, against the oracle; counters too."""
+    w, h = 320, 180
+    s = gpu.Scene.load_json(scene_path(scene), w, h)
+    o = oracle.load(scene_path(scene), w, h)
+    if textures:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import make_atlas
+        s.load_atlas()
+        o.set_atlas(make_atlas.atlas())
+        o.set_textures(True)
+    of = oracle.render(o, spp=spp, nthreads=NTHREADS)
+    full = s.render(spp=spp, want=WANT, stats=True, textures=textures)
+    assert_frames_equal(full, of, ctx="counted")
+    st = full["stats"]
+    assert (st["rays"], st["nodes"], st["leaves"], st["tri_tests"]) == tuple(int(x) for x in of["stats"])
+    fast = s.render(spp=spp, want=WANT, stats=False, textures=textures)
+    for k in WANT:
+        assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
+    assert (full["hit_inst"] >= 0).mean() > 0.2

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT, scene_path
+from twin import NTHREADS, assert_frames_equal, mirror_instances
 
 pytestmark = pytest.mark.gpu
 
@@ -96,15 +97,18 @@ def _move(s, k, inst):
 
 
 @pytest.mark.parametrize("depth", [1, 3])
-def test_pipeline_moving_instances(gpu, depth):
+def test_pipeline_moving_instances(gpu, oracle, depth):
     """rt_builder_set_trans between frames in flight: every frame of the
-    pipeline equals the serial render of the same poses; a debug_cast side entry in the
-    middle (it rebuilds the current slot's BVH) disturbs no frame."""
+    pipeline equals the serial render of the same poses, and the serial frames equal the
+    oracle's render of those poses (including the frames with a 45-degree rotated instance:
+    the general-pose kernels); a debug_cast side entry in the middle (it rebuilds the current
+    slot's BVH) disturbs no frame."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
     import rtamd.dist as rtdist
     w, h, spp, n_frames = 160, 120, 2, 9
     ser = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    o = oracle.load(scene_path("world8_stress"), w, h)
     inst = ser.export("instances").copy()
     refs = []
     for k in range(n_frames):
@@ -112,6 +116,12 @@ def test_pipeline_moving_instances(gpu, depth):
         buf = torch.zeros((h, w), dtype=torch.int32, device="cuda")
         ser.render_device(spp=spp, rgba_ptr=buf.data_ptr(), sync=True)
         refs.append(buf)
+        if depth == 1:                                              # the oracle once per pose sequence
+            mirror_instances(ser, o)
+            of = oracle.render(o, spp=spp, nthreads=NTHREADS)
+            fr = ser.render(spp=spp, want=("rgba", "radiance", "hit_inst", "hit_tri"), stats=False)
+            assert np.array_equal(fr["rgba"], buf.cpu().numpy().view(np.uint32)), k
+            assert_frames_equal(fr, of, ctx=k)
     assert not all(torch.equal(refs[0], r) for r in refs[1:])   # the poses change the frames
     s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
     s.set_frame_slots(depth)

@@ -13,8 +13,19 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN, scene_path
+from twin import NTHREADS, Twin, assert_frames_equal, mirror_camera
 
 pytestmark = pytest.mark.gpu
+WANT = ("rgba", "radiance", "hit_inst", "hit_tri")
+
+
+def orc_check(oracle, o, fr, spp, row0=0, row_step=1, compact=False, use_bvh=1, ctx=""):
+    """fr (a product frame) against the oracle's render of the same rows of scene o."""
+    of = oracle.render(o, spp=spp, use_bvh=use_bvh, row0=row0, row_step=row_step, nthreads=NTHREADS)
+    if compact:
+        of = {k: (v[row0::row_step] if k != "stats" else v) for k, v in of.items()}
+    assert_frames_equal(fr, of, keys=[k for k in WANT if k in fr], ctx=ctx)
+    return of
 
 RAD_RTOL = 1e-5
 
@@ -95,19 +106,22 @@ def test_row_slices_compose(gpu, G, spp):
 
 
 def test_camera_move_rerender(gpu, oracle):
-    """Interactive camera (main.cc:140-180): after translate/rotate the frame still matches the oracle
-    rendering of the same camera pose."""
-    s = gpu.Scene.load_json(scene_path("world8"), 128, 96)
-    s.translate_camera([0.5, -2.0, 1.0])
+    """Interactive camera (main.cc:140-180): after each translate / rotate the frame (counted
+    and fast kernels) equals the oracle's render of the same camera pose."""
     import math
-    a = 0.05
-    s.rotate_camera([math.sin(a / 2), 0, 0, math.cos(a / 2)])
-    fr = s.render(want=("rgba", "hit_inst"))
-    # The oracle has no camera setter: compare against the reference semantics through
-    # invariants instead — the image changed and it is still a valid render.
-    s2 = gpu.Scene.load_json(scene_path("world8"), 128, 96)
-    assert not np.array_equal(fr["rgba"], s2.render()["rgba"])
-    assert (fr["hit_inst"] >= -1).all() and fr["hit_inst"].max() < s.info()["n_instances"]
+    s = gpu.Scene.load_json(scene_path("world8"), 128, 96)
+    o = oracle.load(scene_path("world8"), 128, 96)
+    first = s.render(want=("rgba",))["rgba"]
+    for d, a in (([0.5, -2.0, 1.0], 0.05), ([0.0, 0.0, 3.0], -0.2), ([-1.0, 0.5, 0.0], 0.7)):
+        s.translate_camera(d)
+        s.rotate_camera([math.sin(a / 2), 0, 0, math.cos(a / 2)])
+        mirror_camera(s, o)
+        for stats in (True, False):
+            fr = s.render(spp=2, want=WANT, stats=stats)
+            of = orc_check(oracle, o, fr, 2, ctx=(d, a, stats))
+        if stats:
+            assert tuple(fr["stats"][k] for k in ("rays", "nodes", "leaves", "tri_tests")) == tuple(int(x) for x in of["stats"])
+    assert not np.array_equal(fr["rgba"], first)
 
 
 def test_debug_cast_log(gpu):
@@ -152,6 +166,7 @@ def test_fast_kernel_exact_close_camera(gpu, oracle):
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     _, rot = s.camera()
     # the cubes fill x, z in [-4, 3], y in [0, 11]; the camera looks down at ~58 degrees
+    o = oracle.load(scene_path("world8_stress"), 200, 150)
     for pos in ([0.5, 14.0, -0.5], [0.37, 6.21, -1.13], [-3.9, 10.5, 2.9], [0.0, 3.0, -6.5]):
         s.set_camera(pos, rot)
         fast = s.render(spp=2, want=want, stats=False)
@@ -159,14 +174,17 @@ def test_fast_kernel_exact_close_camera(gpu, oracle):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+        mirror_camera(s, o)
+        orc_check(oracle, o, fast, 2, ctx=pos)
 
 
-def test_fast_kernel_exact_grazing_rays(gpu):
+def test_fast_kernel_exact_grazing_rays(gpu, oracle):
     """Distance pruning and the triangle skip near their worst case: level cameras placed
     exactly on cube face planes and edges (faces at k +- 0.4995), so rays graze faces and
     run along edges at shallow angles, where the slack's max|1/d| factor matters."""
     import math
     s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    o = oracle.load(scene_path("world8_stress"), 160, 120)
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     e = 0.4995
     for pos, yaw in (([e, 3 + e, -8.0], 0.0), ([-1.0, 5 + e, -7.3], 0.0), ([e, 3 + e, -8.0], 1e-3),
@@ -177,15 +195,18 @@ def test_fast_kernel_exact_grazing_rays(gpu):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, yaw, k)
         assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+        mirror_camera(s, o)
+        orc_check(oracle, o, fast, 2, ctx=(pos, yaw))
 
 
-def test_fast_kernel_exact_zero_direction_axes(gpu):
+def test_fast_kernel_exact_zero_direction_axes(gpu, oracle):
     """Zero-direction-axis cut (closest_hit): rays with d_x == 0 (centre column, sample 0)
     and d_y == 0 (centre row) from origins on and around cube face planes, offset by
     fractions and multiples of the pruning slack (~1.4e-3 here), so leaves whose slab is
     skipped by the reference sit just inside and just outside the cut.  Every shadow ray
     of world8_stress's directional light (0, -1, 1) has d_x == 0 as well."""
     s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    o = oracle.load(scene_path("world8_stress"), 160, 120)
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     e = 0.4995
     for off in (0.0, 1e-6, -1e-6, 7e-4, -7e-4, 1.4e-3, -1.4e-3, 3e-3, -3e-3):
@@ -196,15 +217,18 @@ def test_fast_kernel_exact_zero_direction_axes(gpu):
             for k in want:
                 assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, k)
             assert (full["hit_inst"] >= 0).mean() > 0.05, pos          # (a centre row may run in a gap)
+            mirror_camera(s, o)
+            orc_check(oracle, o, fast, 2, ctx=pos)
 
 
-def test_fast_kernel_exact_tiny_direction_components(gpu):
+def test_fast_kernel_exact_tiny_direction_components(gpu, oracle):
     """Rays outside the filtered slab test's range (0 < |d_a| < 2^-64: ray_inv's exact flag),
     which the fast traversal sends to the exact reference test at every node (NaN
     reciprocals, pair_hit_tt2): level cameras turned by 1e-25..1e-21 rad, so the centre
     column's / row's sample-0 rays carry such a component, among ordinary rays."""
     import math
     s = gpu.Scene.load_json(scene_path("world8_stress"), 160, 120)
+    o = oracle.load(scene_path("world8_stress"), 160, 120)
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     e = 0.4995
     for pos in ([e, 3 + e, -8.0], [-2 - e, 6 - e, -7.5], [0.3, 4.2, -6.0]):
@@ -217,14 +241,17 @@ def test_fast_kernel_exact_tiny_direction_components(gpu):
             for k in want:
                 assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, ax, ang, k)
             assert (full["hit_inst"] >= 0).mean() > 0.05, pos
+            mirror_camera(s, o)
+            orc_check(oracle, o, fast, 2, ctx=(pos, ax, ang))
 
 
-def test_fast_kernel_exact_random_cameras(gpu):
+def test_fast_kernel_exact_random_cameras(gpu, oracle):
     """Fast kernel (ordered LBVH, pruning, axis-plane triangle path with its shared-plane
     skip and in-plane reject) == counted reference-heap kernel, bit for bit, from seeded
     random camera poses in and around the cube field (any orientation)."""
     rng = np.random.default_rng(1234)
     s = gpu.Scene.load_json(scene_path("world8_stress"), 96, 64)
+    o = oracle.load(scene_path("world8_stress"), 96, 64)
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     lit = 0.0
     for _ in range(16):
@@ -237,6 +264,8 @@ def test_fast_kernel_exact_random_cameras(gpu):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, k)
         lit += (full["hit_inst"] >= 0).mean()
+        mirror_camera(s, o)
+        orc_check(oracle, o, fast, 2, ctx=pos)
     assert lit / 16 > 0.1
 
 
@@ -263,16 +292,18 @@ def test_timed_frames(gpu):
     assert s.timing_collect()["frames"] == 0
 
 
-@pytest.mark.parametrize("spp", [8, 3])
-def test_fast_kernel_exact_spp8_sky_and_horizon(gpu, spp):
+@pytest.mark.parametrize("spp,w,h", [(8, 240, 160), (3, 240, 160), (16, 160, 120), (64, 64, 48)])
+def test_fast_kernel_exact_spp8_sky_and_horizon(gpu, oracle, spp, w, h):
     """The bench's sample mapping (8 samples per pixel: one-round-trip exchange, clamp before
     the exchange) and the whole-group miss test: fast frames == counted frames bit for bit
     with the camera at the scene's pose, turned to the sky (every group a miss group), at
     the horizon (groups straddling it) and from random poses; with every output, and with
-    the colour alone (the raw-sum exchange skipped).  spp = 3 takes the generic exchange."""
+    the colour alone (the raw-sum exchange skipped).  spp = 3 takes the generic exchange; spp =
+    16 two pixels per lane row, spp = 64 one pixel per wave (config 5's mapping, 1 x 1 sky
+    cones).  Every pose is also put against the oracle."""
     import torch
-    w, h = 240, 160
     s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    o = oracle.load(scene_path("world8_stress"), w, h)
     pos0, q0 = s.camera()
     rng = np.random.default_rng(77)
     poses = [(pos0, q0), (pos0, (-0.3826834, 0.0, 0.0, 0.9238795)), (pos0, (0.0, 0.0, 0.0, 1.0)),
@@ -292,6 +323,8 @@ def test_fast_kernel_exact_spp8_sky_and_horizon(gpu, spp):
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, q, k)
         s.render_device(spp=spp, rgba_ptr=buf.data_ptr(), compact=False, sync=True)
         assert np.array_equal(buf.cpu().numpy().view(np.uint32), full["rgba"]), (pos, q)
+        mirror_camera(s, o)
+        orc_check(oracle, o, fast, spp, ctx=(pos, q))
         hit = full["hit_inst"] >= 0
         sky_seen |= bool((~hit).all())
         lit_seen |= bool(hit.any() and (~hit).any())
@@ -308,15 +341,16 @@ def _scene_bounds(s):
     return lo, hi
 
 
-@pytest.mark.parametrize("spp,row_step", [(8, 1), (2, 1), (8, 3)])
-def test_sky_prepass_grazing_cones(gpu, spp, row_step):
+@pytest.mark.parametrize("spp,row_step", [(8, 1), (2, 1), (8, 3), (16, 1), (64, 2)])
+def test_sky_prepass_grazing_cones(gpu, oracle, spp, row_step):
     """The sky pre-pass decides most groups by their ray cone (cone_misses_root: side planes
     and box faces with conservative margins) and writes their outputs itself.  Cameras on and
     just beside the scene's bounding planes, looking along them, put group cones within
     rounding of the root boxes: fast frames (pre-pass) == counted frames (no pre-pass) bit
     for bit, whole frames and row slices."""
-    w, h = 64, 48
+    w, h = (64, 48) if spp <= 16 else (32, 24)
     s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    o = oracle.load(scene_path("world8_stress"), w, h)
     lo, hi = _scene_bounds(s)
     mid = 0.5 * (lo + hi)
     c, sn = np.cos, np.sin
@@ -339,12 +373,15 @@ def test_sky_prepass_grazing_cones(gpu, spp, row_step):
                     full = s.render(stats=True, **kw)
                     for k in want:
                         assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (axis, side, off, q, k)
+                    mirror_camera(s, o)
+                    orc_check(oracle, o, fast, spp, row0=row_step - 1, row_step=row_step, compact=True,
+                              ctx=(axis, side, off, q))
                     n += 1
     assert n > 60
 
 
 @pytest.mark.parametrize("col1", [(0.9, 0.8, 0.7, 1.0), (0.9, -0.0, 0.7, 1.0)])
-def test_unlit_skip_exact(gpu, col1):
+def test_unlit_skip_exact(gpu, oracle, col1):
     """The fast kernels trace no shadow segments for a light whose phong factor (diffuse +
     specular) is zero in every channel; the light's term is then that signed zero whatever the
     shadow, so frames equal the counted kernel's (every shadow ray traced) bit for bit.  A
@@ -357,7 +394,7 @@ def test_unlit_skip_exact(gpu, col1):
             m(Ka=(0.1, 0.1, 0.1, 1), Kd=(0.2, 0.5, 0.2, 1), Ks=(0.8, 0.8, 0.8, 1), alpha=0.3),
             m(Kd=(0.2, 0.2, 0.6, 1), Kt=(0.5, 0.6, 0.7, 1), eta=1.3),
             m(Kd=(0.3, 0.3, 0.3, 1), Ks=(0.5, 0.5, 0.5, 1), Kr=(0.7, 0.7, 0.7, 1), alpha=8.0)]
-    s = gpu.Scene.create()
+    s = Twin(gpu, oracle)
     meshes = [s.build_cube(1.0, mt) for mt in mats]
     rng = np.random.default_rng(5)
     for i in range(5):
@@ -369,6 +406,7 @@ def test_unlit_skip_exact(gpu, col1):
     s.add_directional_light((-0.2, 1.0, -0.4), (0.4, 0.5, 0.6, 1.0))   # from below
     s.finish(96, 64, 60.0, 100.0, cam_pos=(0.0, 9.0, -9.0), cam_quat=(-0.3826834, 0.0, 0.0, 0.9238795),
              dist_atten=(0.1, 0.05, 0.01), ambience=(0.2, 0.2, 0.2, 1.0), depth=3)
+    o, s = s.orc, s.gpu
     want = ("rgba", "radiance", "hit_inst", "hit_tri")
     poses = [((0.0, 9.0, -9.0), (-0.3826834, 0.0, 0.0, 0.9238795))]
     for _ in range(6):
@@ -383,4 +421,7 @@ def test_unlit_skip_exact(gpu, col1):
         for k in want:
             assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pos, q, k)
         lit += (full["hit_inst"] >= 0).mean()
+        mirror_camera(s, o)
+        of = orc_check(oracle, o, full, 4, ctx=(pos, q))
+        assert tuple(full["stats"][k] for k in ("rays", "nodes", "leaves", "tri_tests")) == tuple(int(x) for x in of["stats"])
     assert lit / len(poses) > 0.05

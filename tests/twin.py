@@ -1,0 +1,69 @@
+"""Test helpers: one scene built twice -- on the product (rtamd, the C ABI) and on the
+oracle (oracle/liboracle.so) -- by the same SceneBuilder calls, and poses mirrored from the
+product to the oracle, so that frames from any camera / instance pose or built scene can be
+compared with the oracle.  TEST INFRASTRUCTURE (may use the oracle)."""
+import os
+
+import numpy as np
+
+NTHREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+
+
+class Twin:
+    """Forwards every SceneBuilder call (scene_builder.h:29-117) to both scenes; index
+    results must agree."""
+
+    def __init__(self, rt, oracle, atlas=""):
+        self.gpu = rt.Scene.create(atlas)
+        self.orc = oracle.create()
+
+    def __getattr__(self, name):
+        if name not in ("add_vertex", "create_mesh", "add_triangle", "add_trans", "build_cube",
+                        "add_point_light", "add_directional_light", "finish", "set_trans"):
+            raise AttributeError(name)
+
+        def call(*a, **k):
+            r0 = getattr(self.gpu, name)(*a, **k)
+            r1 = getattr(self.orc, name)(*a, **k)
+            if r0 is not None or r1 is not None:
+                assert r0 == r1, (name, r0, r1)
+            return r0
+        return call
+
+
+def mirror_camera(gpu_scene, orc_scene):
+    """The product camera's current pose (after translate / rotate / set) on the oracle."""
+    p, q = gpu_scene.camera()
+    orc_scene.set_camera(p, q)
+
+
+def mirror_instances(gpu_scene, orc_scene):
+    """Every instance pose of the product scene on the oracle scene."""
+    inst = gpu_scene.export("instances")
+    for t, row in enumerate(inst):
+        orc_scene.set_trans(t, pos=row[4:7], quat=row[0:4])
+
+
+def orc_render(oracle, orc_scene, **kw):
+    kw.setdefault("nthreads", NTHREADS)
+    return oracle.render(orc_scene, **kw)
+
+
+def assert_frames_equal(gpu_fr, orc_fr, keys=("rgba", "radiance", "hit_inst", "hit_tri"), rtol=1e-5, ctx=""):
+    """The parity bar (BASELINE north_star): hit ids bit-exact, radiance within 1e-5 relative,
+    RGBA8 bytes within 1 where a 1-ulp radiance difference (pow) crosses a byte boundary, on
+    fewer than 1e-3 of the bytes."""
+    for k in ("hit_inst", "hit_tri"):
+        if k in keys:
+            assert np.array_equal(gpu_fr[k], orc_fr[k]), (ctx, k, int((gpu_fr[k] != orc_fr[k]).sum()))
+    if "radiance" in keys:
+        a, b = gpu_fr["radiance"].astype(np.float64), orc_fr["radiance"].astype(np.float64)
+        err = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
+        err[a == b] = 0
+        assert err.max() <= rtol, (ctx, float(err.max()))
+    if "rgba" in keys:
+        ga = np.ascontiguousarray(gpu_fr["rgba"]).view(np.uint8).astype(int)
+        oa = np.ascontiguousarray(orc_fr["rgba"]).view(np.uint8).astype(int)
+        d = np.abs(ga - oa)
+        assert d.max() <= 1, (ctx, int(d.max()))
+        assert (d > 0).mean() < 1e-3, (ctx, float((d > 0).mean()))
