@@ -2518,7 +2518,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.div_perq = udiv_make((unsigned)((P.n_groups + NQ - 1) / NQ));
     P.work = s->d_work; P.tpc = TPC;
     {   // unlit skip (trace_sample, ST_LIGHT): every incoming light must be >= +0 and finite
-        bool ok = !want_stats && !dbg && !prof;
+        bool ok = !want_stats && !dbg;                        // (the PROF variant profiles the fast frame: on)
         auto pos0 = [](float v) { return std::isfinite(v) && !std::signbit(v); };
         for (const DLight& l : h.d_lights) ok = ok && pos0(l.col.x) && pos0(l.col.y) && pos0(l.col.z) && pos0(l.col.w);
         for (const DMat& m : h.d_mats)
@@ -2558,8 +2558,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
                       : (ns <= 2 ? (const void*)trace_kernel<2, true, TF> : (const void*)trace_kernel<NG, true, TF>);
     } else if (tex) {
         fn = textured[use_lds ? 1 : 0][mode];
-    } else if (ft && park && S.tri_ax && prof && ns == 2) {
-        fn = (const void*)trace_kernel<2, true, M_PARK | M_FT | M_AXIS | M_PROF>;
+    } else if (ft && park && S.tri_ax && prof) {
+        constexpr int PP = M_PARK | M_FT | M_AXIS | M_PROF;
+        fn = ns <= 0 ? (const void*)trace_kernel<0, true, PP> : ns <= 2 ? (const void*)trace_kernel<2, true, PP>
+                                                                 : (const void*)trace_kernel<NG, true, PP>;
     } else if (ft && park && S.tri_ax && shade) {
         constexpr int PS = M_PARK | M_FT | M_AXIS | M_SHADE;
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, PS> : ns <= 2 ? (const void*)trace_kernel<2, true, PS>
@@ -3180,6 +3182,44 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         return RT_OK;
     }
     return fail(RT_ERR_ARG, "experiment: 4 (counted, occlusion exit), 5 (counted), 6 (fast kernel, PROF counters)");
+}
+
+int rt_frame_work(rt_scene* s, const rt_render_opts* o, rt_work* w) {
+    CHECK_FINISHED(s);
+    if (!o || !w) return fail(RT_ERR_ARG, "null argument");
+    if (o->spp < 1 || o->spp > 64 || o->row_step < 1 || o->row0 < 0 || !o->use_bvh || o->textures)
+        return fail(RT_ERR_ARG, "rt_frame_work: BVH frames, 1 <= spp <= 64, untextured");
+    int r;
+    if ((r = upload(s)) != RT_OK) return r;
+    HIPCHK(hipSetDevice(s->device));
+    if ((r = ensure_spp(s, o->spp)) != RT_OK) return r;
+    const size_t rows = (s->h.cam.H > o->row0) ? (size_t)(s->h.cam.H - o->row0 + o->row_step - 1) / o->row_step : 0;
+    uint32_t* d_rgba = nullptr;
+    HIPCHK(hipMalloc((void**)&d_rgba, std::max<size_t>(1, (o->compact ? rows : (size_t)s->h.cam.H) * s->h.cam.W) * 4));
+    hipStream_t st = sstream(s);
+    r = begin_frame(s, st, true);                             // nothing else in flight on this slot
+    if (r == RT_OK) r = build_bvh(s, st);
+    if (r == RT_OK) {
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st));
+        HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), st));
+        HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), st));
+        rt_render_opts oo = *o;
+        oo.radiance = nullptr; oo.hit_inst = oo.hit_tri = nullptr;
+        r = launch_trace(s, oo, st, d_rgba, nullptr, -1, -1, false, -1, nullptr, nullptr, true);
+    }
+    if (r == RT_OK) r = end_frame(s, st);
+    unsigned long long v[22] = {};
+    if (r == RT_OK) {
+        HIPCHK(hipStreamSynchronize(st));
+        HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
+        if (v[4] == 0 && rows > 0) r = fail(RT_ERR_STATE, "no profiling variant of the fast kernel for this scene");
+    }
+    (void)hipFree(d_rgba);
+    if (r != RT_OK) return r;
+    w->queries = v[0]; w->wave_queries = v[4]; w->pair_steps = v[5]; w->leaf_visits = v[6]; w->tri_iters = v[7];
+    w->leaf_lanes = v[2];
+    w->scene_bytes = lds_bytes(view_of(s, true), true, true);   // the scene image a block stages
+    return RT_OK;
 }
 
 // Profiling aid (tools/group_profile.py, not on the product path): per-group durations

@@ -35,7 +35,7 @@ SYMBOLS = [
     "rt_render_opts_default", "rt_render", "rt_update_scene", "rt_canvas_read", "rt_canvas_host_ptr",
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
-    "rt_scene_atlas_info", "rt_scene_set_frame_slots",
+    "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_frame_work",
 ]
 
 
@@ -60,6 +60,15 @@ class Stats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Work(ctypes.Structure):
+    _fields_ = [("queries", ctypes.c_uint64), ("wave_queries", ctypes.c_uint64), ("pair_steps", ctypes.c_uint64),
+                ("leaf_visits", ctypes.c_uint64), ("leaf_lanes", ctypes.c_uint64), ("tri_iters", ctypes.c_uint64),
+                ("scene_bytes", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
 _lib = None
@@ -116,6 +125,7 @@ def lib():
     L.rt_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ip)]
     L.rt_device_count.argtypes = [ctypes.POINTER(ip)]
     L.rt_scene_set_frame_slots.argtypes = [vp, ip]
+    L.rt_frame_work.argtypes = [vp, ctypes.POINTER(RenderOpts), ctypes.POINTER(Work)]
     _lib = L
     return L
 
@@ -359,6 +369,16 @@ class Scene:
         st = Stats()
         _check(lib().rt_render(self._h, ctypes.byref(o), ctypes.byref(st) if stats else None))
         return st.as_dict() if stats else None
+
+    def frame_work(self, spp=1, row0=0, row_step=1, compact=True):
+        """What the fast kernels do for this frame (rt_frame_work): queries issued after the
+        exact skips, wave-level traversal steps."""
+        o = RenderOpts()
+        lib().rt_render_opts_default(ctypes.byref(o))
+        o.spp, o.row0, o.row_step, o.compact = spp, row0, row_step, int(compact)
+        w = Work()
+        _check(lib().rt_frame_work(self._h, ctypes.byref(o), ctypes.byref(w)))
+        return w.as_dict()
 
     def set_frame_slots(self, n):
         """1 (default) to 4: consecutive frames rotate through n copies of the per-frame

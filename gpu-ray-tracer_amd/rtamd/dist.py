@@ -110,9 +110,17 @@ class FramePipeline:
       - frame k's render waits for frame k-depth's gather (it rewrites that slice buffer);
       - frame k's gather waits for frame k-depth's un-permute (same gather buffer);
       - frame k's un-permute waits for frame k's gather.
-    Images are the ones serial frames give; only the overlap changes."""
+    Images are the ones serial frames give; only the overlap changes.
 
-    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2):
+    readback=True keeps the reference's post-condition (update_scene returns with the frame
+    host-readable, raytracer.cu:102-120 / canvas.cu:23-29) without giving up the overlap: the
+    finished frame (rank 0) is copied into pinned host buffer k % depth by an asynchronous
+    device-to-host copy -- on the render stream for one rank, on a copy stream after the
+    un-permute otherwise -- while later frames render.  `host_frame(k)` waits for frame k's
+    copy; a host buffer is reused depth frames later, after its copy (and the caller's read)
+    is done."""
+
+    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
@@ -121,10 +129,20 @@ class FramePipeline:
         self.main = torch.cuda.current_stream(device)
         self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(D)]
                       if (world > 1 and rank == 0) else None)
-        self.out = torch.empty((height, width), dtype=dtype, device=device) if (world > 1 and rank == 0) else None
+        self.readback = bool(readback) and (world == 1 or rank == 0)
+        n_out = D if self.readback else 1                 # one un-permute target per slot when copied out
+        self.outs = ([torch.empty((height, width), dtype=dtype, device=device) for _ in range(n_out)]
+                     if (world > 1 and rank == 0) else None)
+        self.out = self.outs[0] if self.outs else None
+        if self.readback:
+            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=True) for _ in range(D)]
+            self.host_ev = [None] * D       # D2H copy of the frame last copied into each host buffer
+            self.host_no = [-1] * D         # its frame number
+            self.copy_stream = torch.cuda.Stream(device=device) if world > 1 else None
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
         self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
+        self.pend_no = [-1] * D         # its frame number
         self.last = -1
 
     @property
@@ -134,6 +152,16 @@ class FramePipeline:
             return self.parts[self.last % self.depth] if self.last >= 0 else None
         return self.out
 
+    def _to_host(self, s, k, src, stream):
+        """Frame k (device buffer src, complete on `stream`) -> pinned host buffer s."""
+        if self.host_ev[s] is not None:
+            self.host_ev[s].synchronize()           # frame k - depth's copy is done (and was read)
+        with torch.cuda.stream(stream):
+            self.host[s].copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self.host_ev[s], self.host_no[s] = ev, k
+
     def _unpermute(self, s):
         if not self.pending[s]:
             return
@@ -142,14 +170,21 @@ class FramePipeline:
             self.work[s].wait()
             if self.rank == 0:
                 g = self.gbufs[s]
+                out = self.outs[s % len(self.outs)]
+                if self.readback and self.host_ev[s] is not None:
+                    self.main.wait_event(self.host_ev[s])   # frame k - depth's copy has read out
                 if self.H % self.world == 0:
-                    self.out.view(self.rows, self.world, self.W).copy_(g.transpose(0, 1))
+                    out.view(self.rows, self.world, self.W).copy_(g.transpose(0, 1))
                 else:
                     for r in range(self.world):
-                        self.out[r::self.world] = g[r][:len(rows_of(r, self.world, self.H))]
+                        out[r::self.world] = g[r][:len(rows_of(r, self.world, self.H))]
+                self.out = out
                 ev = torch.cuda.Event()
                 ev.record(self.main)
                 self.unperm[s] = ev
+                if self.readback:
+                    self.copy_stream.wait_event(ev)
+                    self._to_host(s, self.pend_no[s], out, self.copy_stream)
 
     def step(self, k, render):
         """Issue frame k: render(part, stream) enqueues the render of this rank's rows."""
@@ -159,15 +194,28 @@ class FramePipeline:
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
             render(self.parts[s], st)
+            if self.readback and self.world == 1:
+                self._to_host(s, k, self.parts[s], st)
             if self.world > 1:
                 if self.unperm[s] is not None:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]
                 gl = list(self.gbufs[s].unbind(0)) if self.rank == 0 else None
                 self.work[s] = self.dist.gather(self.parts[s], gl, dst=0, async_op=True)
                 self.pending[s] = True
+                self.pend_no[s] = k
         if k >= 1:
             self._unpermute((k - 1) % self.depth)
         self.last = k
+
+    def host_frame(self, k):
+        """Frame k on the host (readback=True; rank 0): waits for its device-to-host copy.
+        Valid until frame k + depth is issued."""
+        s = k % self.depth
+        if self.world > 1 and self.pending[s] and self.pend_no[s] == k:
+            self._unpermute(s)
+        assert self.host_no[s] == k, (k, self.host_no[s])
+        self.host_ev[s].synchronize()
+        return self.host[s]
 
     def finish(self):
         """Complete every issued frame (stream-ordered on the main stream)."""

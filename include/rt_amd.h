@@ -139,6 +139,26 @@ typedef struct rt_stats {
 void rt_render_opts_default(rt_render_opts* o);
 int rt_render(rt_scene* s, const rt_render_opts* opts, rt_stats* stats);
 
+/* The work the fast (statistics-free) kernels do for one frame of `opts`, from a profiling
+ * run of the fast kernel with wave-level counters (not timed, outputs discarded).  rt_stats
+ * counts the reference's units (every cast_ray of propagate_ray, raytracer.cu:17-43); the
+ * fast kernel proves some of them unnecessary and skips them (unlit shadow rays, pruned
+ * subtrees, occluded-shadow early exits): this is what it does instead. */
+typedef struct rt_work {
+    uint64_t queries;       /* closest-hit queries issued: one per primary sample, reflection /
+                               refraction ray and traced shadow segment */
+    uint64_t wave_queries;  /* wave-level query steps (64 lanes each) */
+    uint64_t pair_steps;    /* wave-level BVH child-pair tests */
+    uint64_t leaf_visits;   /* wave-level leaf (instance) visits */
+    uint64_t leaf_lanes;    /* lane-level leaf visits (cast_local calls) */
+    uint64_t tri_iters;     /* wave-level triangle-loop iterations */
+    uint64_t scene_bytes;   /* the scene the fast kernel reads: ordered-tree records, instance records,
+                               triangles, meshes, materials, lights (staged into each block's LDS) */
+} rt_work;
+/* BVH frames with 1 <= spp <= 64, untextured; RT_ERR_STATE when the scene has no profiling
+ * variant (the fast kernel needs the ordered tree in LDS). */
+int rt_frame_work(rt_scene* s, const rt_render_opts* opts, rt_work* work);
+
 /* Frame slots (1 = default, up to 4).  The reference rebuilds its BVH inside every
  * update_scene call (raytracer.cu:103-119), so a frame owns per-frame state: BVH, work
  * counters and scheduling history.  With n slots, consecutive rt_render calls rotate

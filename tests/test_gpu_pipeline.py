@@ -142,3 +142,39 @@ def test_pipeline_moving_instances(gpu, oracle, depth):
     torch.cuda.synchronize()
     for k in range(n_frames):
         assert torch.equal(outs[k], refs[k]), k
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_pipeline_host_readback(gpu, world):
+    """FramePipeline(readback=True): every frame reaches its pinned host buffer through the
+    asynchronous copy (rank 0 of a world-2 split: after the gather and un-permute), equal to
+    the serial frame, while later frames are in flight."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+    import rtamd.dist as rtdist
+    w, h, spp, depth = 200, 151, 2, 3
+    full = _serial(gpu, "world8_stress", w, h, spp).cpu()
+    s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    s.set_frame_slots(depth)
+    if world == 1:
+        pipe = rtdist.FramePipeline(w, h, 1, 0, "cuda", depth=depth, readback=True)
+        kw = dict(row0=0, row_step=1)
+    else:
+        r1 = _serial(gpu, "world8_stress", w, h, spp, 1, 2)
+        other = torch.zeros((rtdist.slice_height(2, h), w), dtype=torch.int32, device="cuda")
+        other[:r1.shape[0]] = r1
+        pipe = rtdist.FramePipeline(w, h, 2, 0, "cuda", _TwoRankGather(other), depth=depth, readback=True)
+        kw = dict(row0=0, row_step=2)
+    seen = 0
+    for k in range(8):
+        pipe.step(k, lambda buf, st: s.render_device(spp=spp, compact=True, rgba_ptr=buf.data_ptr(),
+                                                     stream=st.cuda_stream, **kw))
+        if k >= depth - 1:
+            j = k - depth + 2 if world > 1 else k - depth + 1
+            if j >= 0:
+                assert torch.equal(pipe.host_frame(j), full), (k, j)
+                seen += 1
+    pipe.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(pipe.host_frame(7), full)
+    assert seen >= 4
