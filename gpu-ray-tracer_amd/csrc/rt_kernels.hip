@@ -886,7 +886,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
     }
     auto pop = [&]() {
         top--;
-        if (top >= 0) { cur = stk[top].f; fl |= 4; }
+        if (NS > 0 && top >= 0) { cur = stk[top].f; fl |= 4; }
     };
     unsigned long long c_post = 0;
     for (;;) {
@@ -952,8 +952,15 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                 if (m.reflective) {
                     dbg(P, me, 2);
                     const V3 hp = at(cur.ray, is_time);
-                    stk[top].f = cur; stk[top].hit_pt = hp; stk[top].norm = is_norm;
-                    top++;
+                    // NS = 0 with depth > 0: the host picks it only when no material is refractive.
+                    // The suspended frame would then only be popped when resumed (its REFRACT step
+                    // pops: the material of the shared Isect is never refractive, scene.cu:149-184),
+                    // and so would every frame under it, so the child replaces it (a tail call):
+                    // no stack, no scratch writes.
+                    if (NS > 0) {
+                        stk[top].f = cur; stk[top].hit_pt = hp; stk[top].norm = is_norm;
+                        top++;
+                    }
                     cur.type = F_NORMAL;                           // the child: last_mat, in_obj inherited
                     cur.atten = cur.atten * m.Kr;
                     cur.depth = cur.depth - 1;
@@ -2533,7 +2540,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const bool ft = mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
     const size_t lds = lds_bytes(S, ft);
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
-    const int ns = h.depth;                                   // suspended frames needed (<= MAX_FRAMES - 1)
+    // suspended frames needed (<= MAX_FRAMES - 1); none without a refractive material, where a
+    // reflection child replaces its parent (trace_sample, F_REFLECT)
+    const int ns = opaque_scene(s) ? 0 : h.depth;
     const void* fn;
     const int mode = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     constexpr int NG = MAX_FRAMES - 1;                     // generic frame-stack depth
