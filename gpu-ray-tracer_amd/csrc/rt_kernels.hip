@@ -34,11 +34,13 @@
 #include <string>
 #include <vector>
 
+#include "rt_bvh.h"
 #include "rt_math.h"
 #include "rt_scene.h"
 #include "../../include/rt_amd.h"
 
 using namespace rtm;
+using namespace rtb;
 using rt::DCamera;
 using rt::DInst;
 using rt::DLight;
@@ -50,7 +52,8 @@ using rt::DTri;
 namespace {
 
 constexpr int MAX_FRAMES = 10;           // renv::gpu::MAX_DEPTH (scene.cu:25)
-constexpr int BVH_MAX_LEAVES = 8192;     // single-workgroup BVH build limit (LDS keys)
+constexpr int BVH_WG_LEAVES = 8192;      // single-workgroup BVH build (LDS keys); above: bvh_build_large
+constexpr int BVH_MAX_LEAVES = 1 << 24;  // padded leaves (int indexing of the 12n-float pair records)
 #ifndef RT_BLOCK
 #define RT_BLOCK 1024
 #endif
@@ -1619,80 +1622,6 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
 // BVH build: ropt::gpu::BVH::BVH (bvh.cu:74-91) + create_boxes (raytracer.cu:54-74)
 // in one workgroup.  Output: heap-ordered nodes[1 .. 2n-1].
 // ---------------------------------------------------------------------------
-struct BvhArgs {
-    int* work; int n_work;   // the trace kernel's work counters, zeroed here (saves a memset launch)
-    unsigned long long* hctl; // next frame's heavy-list counters (2 words), zeroed here too (may be null)
-    const DInst* insts; int n_inst;
-    const Box* mesh_box;     // per-mesh AABB, Trimesh::compute_bounding_box + the mesh pose (host, static)
-    int n;                   // padded leaf count (power of two)
-    Box* tree;               // 2n-1 boxes, reference storage order (global scratch when the LDS cannot hold it)
-    float* node_pair;        // out: [12n] child-pair layout (BvhRefs); degenerate boxes: min=+inf, max=-inf
-    float4* fnode;           // out: ordered LBVH of the fast kernel, [4 (n_real-1)] (see FNode below)
-    int n_real;              // instances with a non-degenerate box (leaves of the ordered LBVH)
-    int* leaf_inst;          // out: [n] instance of leaf node n+i
-};
-
-// Box storage of the build: the reference's level arrays (bvh.cu:43-61) as SoA columns
-// (mn xyz, mx xyz, nd) in LDS -- conflict-free for consecutive boxes -- or the global
-// Box array for trees too large for the LDS.
-template <bool LDS_TREE> struct TreeStore;
-template <> struct TreeStore<true> {
-    float* f; int cap;
-    __device__ Box get(int i) const {
-        Box b;
-        b.mn = v3(f[i], f[cap + i], f[2 * cap + i]); b.mx = v3(f[3 * cap + i], f[4 * cap + i], f[5 * cap + i]);
-        b.nd = __float_as_int(f[6 * cap + i]);
-        return b;
-    }
-    __device__ void put(int i, const Box& b) {
-        f[i] = b.mn.x; f[cap + i] = b.mn.y; f[2 * cap + i] = b.mn.z;
-        f[3 * cap + i] = b.mx.x; f[4 * cap + i] = b.mx.y; f[5 * cap + i] = b.mx.z;
-        f[6 * cap + i] = __int_as_float(b.nd);
-    }
-};
-template <> struct TreeStore<false> {
-    Box* t;
-    __device__ Box get(int i) const { return t[i]; }
-    __device__ void put(int i, const Box& b) { t[i] = b; }
-};
-// LDS bytes of bvh_build_kernel<LDS_TREE>: keys u64[n] | idx int[n] | (tree 7 x f32 [2n-1])
-__host__ __device__ inline size_t bvh_lds_bytes(int n, bool lds_tree) {
-    return 12 * (size_t)n + (lds_tree ? 28 * (size_t)(2 * n - 1) : 0);
-}
-
-// Karras radix-tree node i over sorted 64-bit keys k[0, nr): range [first, last] and
-// split gamma (left = [first, gamma], right = [gamma+1, last]); equal keys are told
-// apart by their index (delta = 64 + clz(i ^ j)).
-__host__ __device__ inline int fnode_delta(const unsigned long long* k, int nr, int i, int j) {
-    if (j < 0 || j >= nr) return -1;
-    const unsigned long long x = k[i] ^ k[j];
-    if (x == 0) {
-        const unsigned y = (unsigned)(i ^ j);
-        return 64 + (y ? __builtin_clz(y) : 32);
-    }
-    return __builtin_clzll(x);
-}
-__host__ __device__ inline void fnode_split(const unsigned long long* k, int nr, int i, int& first, int& last, int& gamma) {
-    const int d = fnode_delta(k, nr, i, i + 1) - fnode_delta(k, nr, i, i - 1) >= 0 ? 1 : -1;
-    const int dmin = fnode_delta(k, nr, i, i - d);
-    int lmax = 2;
-    while (fnode_delta(k, nr, i, i + lmax * d) > dmin) lmax *= 2;
-    int l = 0;
-    for (int t = lmax / 2; t >= 1; t /= 2)
-        if (fnode_delta(k, nr, i, i + (l + t) * d) > dmin) l += t;
-    const int j = i + l * d;
-    const int dnode = fnode_delta(k, nr, i, j);
-    int sp = 0;
-    for (int div = 2;; div *= 2) {
-        const int t = (l + div - 1) / div;
-        if (fnode_delta(k, nr, i, i + (sp + t) * d) > dnode) sp += t;
-        if (t <= 1) break;
-    }
-    gamma = i + sp * d + (d < 0 ? -1 : 0);
-    first = i < j ? i : j;
-    last = i < j ? j : i;
-}
-
 template <bool LDS_TREE>
 __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1708,14 +1637,9 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
 
     // instance boxes (create_boxes, raytracer.cu:54-74: from_local of the mesh box) and
     // Morton keys (gen_morton, bvh.cu:20-32); padding is degenerate -> ULONG_MAX
-    auto inst_box = [&](int i) {
-        Box b; b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
-        if (i < A.n_inst) b = from_local(A.mesh_box[A.insts[i].mesh], A.insts[i].pose);
-        return b;
-    };
+    auto inst_box = [&](int i) { return bvh_inst_box(A, i); };
     for (int i = tid; i < n; i += nt) {
-        const Box b = inst_box(i);
-        keys[i] = b.nd ? z_order(neg(box_center(b))) : ~0ull;
+        keys[i] = bvh_key(inst_box(i));
         idx[i] = i;
     }
     __syncthreads();
@@ -1829,42 +1753,8 @@ __global__ __launch_bounds__(1024) void bvh_build_kernel(BvhArgs A) {
             lvl += size; out += size / 2; size >>= 1;
         }
     }
-    // heap layout: node k lives at reference storage index 2n-1-k (bvh.h:51-53)
-    for (int k = tid; k < 2 * n; k += nt) {
-        Box b;
-        b.nd = 0;
-        if (k > 0) b = tree.get(2 * n - 1 - k);
-        if (!b.nd) { b.mn = v3(INFINITY, INFINITY, INFINITY); b.mx = v3(-INFINITY, -INFINITY, -INFINITY); }
-        float* q = A.node_pair + 12 * (k >> 1) + (k & 1);
-        q[0] = b.mn.x; q[2] = b.mn.y; q[4] = b.mn.z; q[6] = b.mx.x; q[8] = b.mx.y; q[10] = b.mx.z;
-        if (k >= n) A.leaf_inst[k - n] = idx[2 * n - 1 - k];
-    }
-    // Ordered LBVH (fast kernel): a radix tree (Karras 2012) over the same sorted
-    // leaves.  Internal node i splits at the highest differing key bit; the child
-    // whose leaves are later in storage order is child A (visited first), so
-    // leaves are met in the heap's DFS order (heap leaf k <-> storage 2n-1-k).
-    const int nr = A.n_real;                    // real leaves = storage [0, nr) (padding sorts last)
-    for (int i = tid; i < nr - 1; i += nt) {
-        int first, last, gamma;
-        fnode_split(keys, nr, i, first, last, gamma);
-        const int cl[2] = {gamma + 1, gamma}, lo[2] = {gamma + 1, first}, hi[2] = {last, gamma};
-        float* q = reinterpret_cast<float*>(A.fnode + 4 * (size_t)i);
-        int* refs = reinterpret_cast<int*>(A.fnode + 4 * (size_t)i + 3);
-        for (int c = 0; c < 2; c++) {                   // c = 0: child A (later leaves), 1: child B
-            // box of storage leaves [lo, hi]: the level arrays of A.tree are a segment
-            // tree over storage order, so O(2 log n) aligned blocks cover the range
-            // (min/max merges are exact, any grouping gives the same bounds)
-            Box b;
-            b.nd = 0; b.mn = b.mx = v3(0, 0, 0);
-            for (int l = lo[c], r = hi[c] + 1, off = 0, size = n; l < r; l >>= 1, r >>= 1, off += size, size >>= 1) {
-                if (l & 1) b = merge(b, tree.get(off + l++));
-                if (r & 1) b = merge(b, tree.get(off + --r));
-            }
-            q[0 + c] = b.mn.x; q[2 + c] = b.mn.y; q[4 + c] = b.mn.z; q[6 + c] = b.mx.x; q[8 + c] = b.mx.y; q[10 + c] = b.mx.z;
-            refs[c] = lo[c] == hi[c] ? -1 - idx[lo[c]] : cl[c];      // leaf: -1 - instance
-        }
-        refs[2] = refs[3] = 0;
-    }
+    for (int k = tid; k < 2 * n; k += nt) bvh_heap_node(A, idx, tree, k);
+    for (int i = tid; i < A.n_real - 1; i += nt) bvh_fnode(A, keys, idx, tree, i);
 }
 
 // ---------------------------------------------------------------------------
@@ -1975,6 +1865,7 @@ struct rt_scene {
     DLight* d_lights = nullptr; Box* d_mesh_box = nullptr; Box* d_tree = nullptr;
     float4* d_node_pair = nullptr; int* d_leaf = nullptr;
     float4* d_fnode = nullptr; int n_real = 0, fdepth = 0;   // ordered LBVH (fast kernel)
+    void* d_bscratch = nullptr;                  // bvh_build_large's sort buffers (scenes above BVH_WG_LEAVES)
     float4* d_inst4 = nullptr;
     TriAx* d_tri_ax = nullptr;                   // axis-plane triangle records (tri_axis_records)
     int* d_work = nullptr; int n_cu = 0;
@@ -2018,6 +1909,7 @@ struct rt_scene {
     static constexpr int MAX_SLOTS = RT_MAX_SLOTS;
     struct Slot {
         Box* d_tree = nullptr; float4* d_node_pair = nullptr; int* d_leaf = nullptr; float4* d_fnode = nullptr;
+        void* d_bscratch = nullptr;
         int* d_work = nullptr; bool work_zeroed = false, bvh_valid = false;
         int* d_hlist[2] = {nullptr, nullptr}; unsigned char* d_hflag[2] = {nullptr, nullptr};
         unsigned long long* d_hctl = nullptr;
@@ -2044,6 +1936,7 @@ void select_slot(rt_scene* s, int i) {
     auto move = [&](rt_scene::Slot& o, bool save) {
         auto f = [&](auto& field, auto& slot) { if (save) xfer(slot, field); else xfer(field, slot); };
         f(s->d_tree, o.d_tree); f(s->d_node_pair, o.d_node_pair); f(s->d_leaf, o.d_leaf); f(s->d_fnode, o.d_fnode);
+        f(s->d_bscratch, o.d_bscratch);
         f(s->d_work, o.d_work); f(s->work_zeroed, o.work_zeroed); f(s->bvh_valid, o.bvh_valid);
         for (int p = 0; p < 2; p++) { f(s->d_hlist[p], o.d_hlist[p]); f(s->d_hflag[p], o.d_hflag[p]); }
         f(s->d_hctl, o.d_hctl); f(s->hist_cap, o.hist_cap); f(s->hist_parity, o.hist_parity);
@@ -2240,7 +2133,7 @@ int upload(rt_scene* s) {
         (r = up(s->d_mats, h.d_mats)) || (r = up(s->d_lights, h.d_lights)))
         return r;
     s->n_leaf = padded((int)h.d_insts.size());
-    if (s->n_leaf > BVH_MAX_LEAVES) return fail(RT_ERR_LIMIT, "more than 8192 padded instances: single-workgroup BVH build limit");
+    if (s->n_leaf > BVH_MAX_LEAVES) return fail(RT_ERR_LIMIT, "more than 2^24 padded instances");
     s->n_cu = prop.multiProcessorCount;
     size_t nl = std::max(1, s->n_leaf);
     HIPCHK(hipMalloc((void**)&s->d_node_pair, 3 * nl * sizeof(float4)));
@@ -2431,6 +2324,13 @@ int build_bvh(rt_scene* s, hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e
     // the slot the next fast frame records its heavy list into (launch_trace skips its memset)
     A.hctl = s->d_hctl ? s->d_hctl + 2 * (1 - s->hist_parity) : nullptr;
     s->hctl_zeroed = s->d_hctl ? 1 - s->hist_parity : -1;
+    if (A.n > BVH_WG_LEAVES) {                                // above one workgroup's LDS: the grid-wide build
+        if (!s->d_bscratch) HIPCHK(hipMalloc(&s->d_bscratch, bvh_large_scratch_bytes(A.n)));
+        HIPCHK(bvh_build_large(A, s->d_bscratch, st, e0, e1));
+        s->bvh_valid = true;
+        s->work_zeroed = true;
+        return RT_OK;
+    }
     const bool lds_tree = bvh_lds_bytes(A.n, true) <= 160 * 1024;       // n <= 2048
     const size_t lds = bvh_lds_bytes(A.n, lds_tree);
     if (lds > 160 * 1024) return fail(RT_ERR_LIMIT, "BVH build needs more LDS than one CU has");
@@ -2672,6 +2572,7 @@ rt_scene::~rt_scene() {
     if (uploaded) (void)hipSetDevice(device);
     free_atlas(this);
     dfree(d_fnode);
+    if (d_bscratch) (void)hipFree(d_bscratch);
     for (int p = 0; p < 2; p++) { dfree(d_hlist[p]); dfree(d_hflag[p]); }
     dfree(d_hctl);
     dfree(d_gsky); dfree(d_live);
@@ -2687,6 +2588,7 @@ rt_scene::~rt_scene() {
         if (i == cur_slot) continue;
         Slot& o = store[i];
         dfree(o.d_tree); dfree(o.d_node_pair); dfree(o.d_leaf); dfree(o.d_fnode); dfree(o.d_work);
+        if (o.d_bscratch) (void)hipFree(o.d_bscratch);
         for (int p = 0; p < 2; p++) { dfree(o.d_hlist[p]); dfree(o.d_hflag[p]); }
         dfree(o.d_hctl); dfree(o.d_gsky); dfree(o.d_live);
         dfree(o.d_insts); dfree(o.d_inst4);
