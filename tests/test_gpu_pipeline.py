@@ -45,8 +45,17 @@ def test_frame_slots_streams_identical(gpu, scene, spp, depth):
 
 
 class _Work:
+    """Like a torch.distributed Work: wait() makes the current stream wait for the copies
+    issued on the stream current at the gather."""
+
+    def __init__(self):
+        import torch
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
     def wait(self):
-        pass
+        import torch
+        torch.cuda.current_stream().wait_event(self.ev)
 
 
 class _TwoRankGather:

@@ -19,11 +19,12 @@ import sys
 
 def is_timed_trace(name):
     """The frame kernel bench.py times: trace_kernel<NS, LDS, MODE> without the STATS bit
-    (the single counted frame bench.py renders first uses MODE 2/3)."""
+    (the single counted frame bench.py renders first uses MODE 2/3) and without the PROF bit
+    (rt_frame_work's untimed profiling frame, MODE bit 6)."""
     if "trace_kernel<" not in name:
         return False
     mode = name.split("trace_kernel<", 1)[1].split(">", 1)[0].split(",")[-1].strip()
-    return mode.isdigit() and (int(mode) & 2) == 0          # MODE bit 1 = STATS
+    return mode.isdigit() and (int(mode) & 2) == 0 and (int(mode) & 64) == 0
 
 
 def is_sky(name):
