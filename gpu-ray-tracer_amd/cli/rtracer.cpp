@@ -2,6 +2,7 @@
 //
 //   rtracer -c world8.json [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K]
 //           [--width W --height H] [--out frame.ppm] [--debug X,Y] [--textures [ATLAS.png]]
+//           [--gpus N [--ranks R]]
 //
 // -c config (worldN.json), -b benchmark (one timed frame, "Time: X ms" as main.cc:210-216),
 // -r unoptimize (brute force, no BVH), -d kernel dimension (accepted; the HIP path
@@ -11,7 +12,8 @@
 // (default 1) through rtracer::gpu::update_scene and prints the frame rate.  --spp > 1
 // uses the build's multi-sample extension (rt_render).  --debug X,Y runs debug_cast.
 // --textures turns on the build-defined textured shading mode with the scene's atlas
-// (or the given PNG).
+// (or the given PNG).  --gpus N splits every frame row-cyclically over devices 0..N-1 of this
+// process (R slices, default N; RCCL gather to device 0: rtracer::gpu::use_devices).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -24,7 +26,7 @@
 static void usage() {
     std::fprintf(stderr,
                  "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
-                 "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]]\n");
+                 "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]] [--gpus N [--ranks R]]\n");
 }
 
 static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
@@ -47,7 +49,7 @@ int main(int argc, char** argv) {
     std::string config, out;
     bool bench = false, unopt = false, serial = false, textures = false;
     std::string atlas;
-    int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1;
+    int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1, gpus = 1, ranks = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](const char* name) -> const char* {
@@ -64,6 +66,8 @@ int main(int argc, char** argv) {
         else if (a == "--width") width = std::atoi(val("--width"));
         else if (a == "--height") height = std::atoi(val("--height"));
         else if (a == "--out") out = val("--out");
+        else if (a == "--gpus") gpus = std::atoi(val("--gpus"));
+        else if (a == "--ranks") ranks = std::atoi(val("--ranks"));
         else if (a == "--textures") {
             textures = true;
             if (i + 1 < argc && argv[i + 1][0] != '-') atlas = argv[++i];
@@ -78,7 +82,7 @@ int main(int argc, char** argv) {
                              "restated in oracle/ for testing only\n");
         return 2;
     }
-    if (frames < 1 || spp < 1) { usage(); return 2; }
+    if (frames < 1 || spp < 1 || gpus < 1 || ranks < 0) { usage(); return 2; }
 
     // procedural::gpu::generate with optional canvas override; a bad config is reported
     // and exits (the reference asserts)
@@ -95,6 +99,12 @@ int main(int argc, char** argv) {
     renv::Environment& env = scene->get_environment();
     std::printf("Loaded scene\n");
     const int W = env.get_canvas().get_width(), H = env.get_canvas().get_height();
+    if (gpus > 1 || ranks > 1) {
+        std::vector<int> devs(gpus);
+        for (int d = 0; d < gpus; d++) devs[d] = d;
+        rtracer::gpu::use_devices(scene, devs, ranks > 0 ? ranks : gpus);
+        std::printf("Frames split over %d GPU(s), %d slices\n", gpus, ranks > 0 ? ranks : gpus);
+    }
 
     std::vector<uint32_t> host;
     auto draw = [&]() {

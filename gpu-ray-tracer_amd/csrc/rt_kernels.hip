@@ -20,8 +20,10 @@
 //    with scalar loads, `__ballot` decides descend vs. skip (scene.cu:54-70).
 //    Leaf and box tests use the reference's exact float32 operations, so hit
 //    indices are bit-identical to the single-ray semantics.
+#include <dlfcn.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types only: RCCL is opened at run time (MultiDev), never linked
 
 #include <algorithm>
 #include <cmath>
@@ -1854,8 +1856,10 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
 // ===========================================================================
 // Host side: scene object and the C ABI
 // ===========================================================================
+struct MultiDev;
 struct rt_scene {
     rt::Scene h;
+    MultiDev* multi = nullptr;                   // rt_scene_set_devices: frames split over several GPUs
     bool finished = false;
     int device = -1;
     hipStream_t stream = nullptr;
@@ -2568,7 +2572,9 @@ void invalidate(rt_scene* s) {
 
 }  // namespace
 
+void free_multi(rt_scene* s);
 rt_scene::~rt_scene() {
+    free_multi(this);
     if (uploaded) (void)hipSetDevice(device);
     free_atlas(this);
     dfree(d_fnode);
@@ -2597,6 +2603,207 @@ rt_scene::~rt_scene() {
     for (auto& e : slot_done) if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
 }
+
+// ---------------------------------------------------------------------------
+// Multi-GPU frames from one host process (rt_scene_set_devices).  The frame is
+// split row-cyclically into n_ranks slices (slice r = rows r, r + N, ...), the BVH and scene
+// replicated on every device (each replica rebuilds the same tree from the same instance
+// array, raytracer.cu:103-119), so the one exchange is the gather of the RGBA8 slices:
+//   1. device i renders ranks [i k, (i+1) k) (k = n_ranks / n_devices) into its slice buffer
+//      sbuf[i] = k slices of rows_max x W (compact rows; rows_max = ceil(H / N)), on its stream;
+//   2. ncclGroupStart; per device ncclGather(sbuf[i], gbuf on device 0, k rows_max W uint32,
+//      root 0, comm[i], stream[i]); ncclGroupEnd -- one communicator per device from
+//      ncclCommInitAll, so rank order = device order = slice order;
+//   3. device 0 un-permutes gbuf into the frame (unpermute_kernel).
+// Several ranks per device ("virtual" ranks: n_ranks > n_devices) keep the same sequence, so a
+// one-GPU box runs the whole call sequence with a one-rank communicator.  RCCL is opened
+// with dlopen at the first multi-device frame (the copy torch loaded, if any): the library
+// has no link-time RCCL dependency.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void unpermute_kernel(const uint32_t* __restrict__ g, uint32_t* __restrict__ out, int W,
+                                                        int H, int N, int rows_max) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)W * H) return;
+    const int y = (int)(i / W), x = (int)(i - (long long)y * W);
+    out[i] = g[((size_t)(y % N) * rows_max + y / N) * W + x];         // frame row y = slice y % N, row y / N
+}
+
+struct Rccl {
+    void* lib = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*err)(ncclResult_t) = nullptr;
+};
+Rccl* rccl(std::string* why) {
+    static Rccl R;
+    static std::string reason;
+    static bool tried = false;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!tried) {
+        tried = true;
+        for (const char* n : {"librccl.so", "librccl.so.1"})                 // the copy already loaded (torch's)
+            if (!R.lib) R.lib = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+        for (const char* n : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"})
+            if (!R.lib) R.lib = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+        if (!R.lib) { reason = std::string("cannot load RCCL: ") + dlerror(); }
+        else {
+            auto sym = [&](const char* n) { void* f = dlsym(R.lib, n); if (!f && reason.empty()) reason = std::string("RCCL lacks ") + n; return f; };
+            R.comm_init_all = (decltype(R.comm_init_all))sym("ncclCommInitAll");
+            R.comm_destroy = (decltype(R.comm_destroy))sym("ncclCommDestroy");
+            R.gather = (decltype(R.gather))sym("ncclGather");
+            R.group_start = (decltype(R.group_start))sym("ncclGroupStart");
+            R.group_end = (decltype(R.group_end))sym("ncclGroupEnd");
+            R.err = (decltype(R.err))sym("ncclGetErrorString");
+        }
+    }
+    if (!reason.empty()) { if (why) *why = reason; return nullptr; }
+    return &R;
+}
+}  // namespace
+
+struct MultiDev {
+    std::vector<int> devices;
+    int n_ranks = 1, per_dev = 1, rows_max = 0, W = 0, H = 0;
+    std::vector<rt_scene*> reps;                 // reps[0] = the scene itself; reps[i > 0] owned replicas
+    std::vector<hipStream_t> streams;
+    std::vector<uint32_t*> sbuf;                 // per device: per_dev slices of rows_max x W
+    uint32_t* gbuf = nullptr;                    // device 0: n_ranks slices
+    std::vector<ncclComm_t> comms;
+    std::vector<unsigned> inst_gen;              // host instance generation each replica holds
+};
+
+void free_multi(rt_scene* s) {
+    MultiDev* m = s->multi;
+    if (!m) return;
+    s->multi = nullptr;
+    Rccl* R = rccl(nullptr);
+    for (size_t i = 0; i < m->devices.size(); i++) {
+        (void)hipSetDevice(m->devices[i]);
+        if (i < m->streams.size() && m->streams[i]) { (void)hipStreamSynchronize(m->streams[i]); (void)hipStreamDestroy(m->streams[i]); }
+        if (i < m->sbuf.size() && m->sbuf[i]) (void)hipFree(m->sbuf[i]);
+        if (R && i < m->comms.size() && m->comms[i]) (void)R->comm_destroy(m->comms[i]);
+    }
+    if (m->gbuf) { (void)hipSetDevice(m->devices[0]); (void)hipFree(m->gbuf); }
+    for (size_t i = 1; i < m->reps.size(); i++) delete m->reps[i];
+    if (s->uploaded) (void)hipSetDevice(s->device);
+    delete m;
+}
+
+namespace {
+// Replica i's host scene brought up to the primary's: camera, environment, instance poses,
+// atlas (the device copies follow at its next frame, as for any scene).
+void sync_replica(rt_scene* s, MultiDev* m, size_t i) {
+    rt_scene* r = m->reps[i];
+    r->h.cam = s->h.cam; r->h.d_cam = s->h.d_cam;
+    r->h.dist_atten = s->h.dist_atten; r->h.ambience = s->h.ambience; r->h.depth = s->h.depth;
+    if (m->inst_gen[i] != s->inst_gen) {
+        r->h.insts = s->h.insts; r->h.d_insts = s->h.d_insts;
+        r->inst_gen++;
+        invalidate(r);
+        m->inst_gen[i] = s->inst_gen;
+    }
+    if (r->h.atlas_rgba.size() != s->h.atlas_rgba.size() || (s->atlas_dirty && !s->h.atlas_rgba.empty())) {
+        r->h.atlas_rgba = s->h.atlas_rgba; r->h.atlas_w = s->h.atlas_w; r->h.atlas_h = s->h.atlas_h;
+        r->atlas_dirty = true;
+    }
+}
+
+int render_multi(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
+    MultiDev* m = s->multi;
+    if (o->radiance || o->hit_inst || o->hit_tri) return fail(RT_ERR_ARG, "multi-device frames write RGBA8 only");
+    std::string why;
+    Rccl* R = rccl(&why);
+    if (!R) return fail(RT_ERR_STATE, why);
+    const int nd = (int)m->devices.size(), N = m->n_ranks, W = s->h.cam.W, H = s->h.cam.H;
+    int r;
+    if (m->W != W || m->H != H) return fail(RT_ERR_STATE, "canvas size changed after rt_scene_set_devices");
+    // replicas, streams, buffers and communicators on first use
+    if (m->comms.empty()) {
+        for (int i = 0; i < nd; i++) {
+            HIPCHK(hipSetDevice(m->devices[i]));
+            if (i > 0) {
+                rt_scene* rp = new rt_scene;
+                rp->h = s->h; rp->finished = true;
+                rp->h.atlas_rgba.clear();
+                m->reps.push_back(rp);
+                m->inst_gen.push_back(0);
+                const int saved = g_device;
+                g_device = m->devices[i];
+                r = upload(rp);
+                g_device = saved;
+                if (r != RT_OK) return r;
+            }
+            hipStream_t st;
+            HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            m->streams.push_back(st);
+            uint32_t* b = nullptr;
+            HIPCHK(hipMalloc((void**)&b, (size_t)m->per_dev * m->rows_max * W * 4));
+            m->sbuf.push_back(b);
+        }
+        HIPCHK(hipSetDevice(m->devices[0]));
+        HIPCHK(hipMalloc((void**)&m->gbuf, (size_t)N * m->rows_max * W * 4));
+        m->comms.assign(nd, nullptr);
+        ncclResult_t e = R->comm_init_all(m->comms.data(), nd, m->devices.data());
+        if (e != ncclSuccess) { m->comms.clear(); return fail(RT_ERR_HIP, std::string("ncclCommInitAll: ") + R->err(e)); }
+    }
+    for (int i = 1; i < nd; i++) sync_replica(s, m, i);
+    unsigned long long tot[4] = {0, 0, 0, 0};
+    double bvh_ms = 0, trace_ms = 0;
+    // 1. every rank's slice, on its device's stream
+    for (int i = 0; i < nd; i++)
+        for (int j = 0; j < m->per_dev; j++) {
+            rt_render_opts so = *o;
+            so.row0 = i * m->per_dev + j; so.row_step = N; so.compact = 1;
+            so.rgba = m->sbuf[i] + (size_t)j * m->rows_max * W;
+            so.stream = m->streams[i]; so.host_outputs = 0; so.sync = 0;
+            rt_stats st{};
+            if ((r = rt_render(m->reps[i], &so, stats ? &st : nullptr)) != RT_OK) return r;
+            if (stats) {
+                tot[0] += st.rays; tot[1] += st.nodes; tot[2] += st.leaves; tot[3] += st.tri_tests;
+                bvh_ms = std::max(bvh_ms, st.bvh_ms); trace_ms += st.trace_ms;
+            }
+        }
+    // 2. the gather to device 0 (one communicator per device, grouped)
+    const size_t cnt = (size_t)m->per_dev * m->rows_max * W;
+    ncclResult_t e = R->group_start();
+    for (int i = 0; i < nd && e == ncclSuccess; i++) {
+        HIPCHK(hipSetDevice(m->devices[i]));
+        e = R->gather(m->sbuf[i], i == 0 ? m->gbuf : nullptr, cnt, ncclUint32, 0, m->comms[i], m->streams[i]);
+    }
+    ncclResult_t e2 = R->group_end();
+    if (e == ncclSuccess) e = e2;
+    if (e != ncclSuccess) return fail(RT_ERR_HIP, std::string("ncclGather: ") + R->err(e));
+    // 3. un-permute on device 0 into the caller's buffer or the canvas
+    HIPCHK(hipSetDevice(m->devices[0]));
+    uint32_t* out = (o->rgba && !o->host_outputs) ? o->rgba : s->d_canvas;
+    const long long px = (long long)W * H;
+    hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, m->streams[0], m->gbuf, out, W, H,
+                       N, m->rows_max);
+    HIPCHK(hipGetLastError());
+    hipStream_t caller = o->stream ? (hipStream_t)o->stream : nullptr;
+    if (caller) {                                          // the caller's stream continues after the frame
+        hipEvent_t ev;
+        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ev, m->streams[0]));
+        HIPCHK(hipStreamWaitEvent(caller, ev, 0));
+        HIPCHK(hipEventDestroy(ev));
+    }
+    if (o->sync || o->host_outputs || stats)
+        for (int i = 0; i < nd; i++) { HIPCHK(hipSetDevice(m->devices[i])); HIPCHK(hipStreamSynchronize(m->streams[i])); }
+    HIPCHK(hipSetDevice(m->devices[0]));
+    if (o->host_outputs && o->rgba) HIPCHK(hipMemcpy(o->rgba, out, (size_t)px * 4, hipMemcpyDeviceToHost));
+    if (stats) {
+        stats->rays = tot[0]; stats->nodes = tot[1]; stats->leaves = tot[2]; stats->tri_tests = tot[3];
+        stats->bvh_ms = bvh_ms; stats->trace_ms = trace_ms;
+    }
+    return RT_OK;
+}
+}  // namespace
 
 extern "C" {
 
@@ -2903,6 +3110,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     if ((r = upload(s)) != RT_OK) return r;
     HIPCHK(hipSetDevice(s->device));
     if ((size_t)s->h.cam.W * s->h.cam.H > (size_t)INT32_MAX) return fail(RT_ERR_LIMIT, "frame larger than 2^31 pixels");
+    if (s->multi && o->row0 == 0 && o->row_step == 1) return render_multi(s, o, stats);   // whole frames: split
     if ((r = ensure_spp(s, o->spp)) != RT_OK) return r;
     hipStream_t st = o->stream ? (hipStream_t)o->stream : sstream(s);
     const bool timed = stats != nullptr;
@@ -2982,6 +3190,41 @@ int rt_scene_set_frame_slots(rt_scene* s, int n) {
     for (auto& p : s->slot_pending) p = false;
     s->n_slots = n;
     return (n > 1 && s->uploaded) ? ensure_other_slot(s) : RT_OK;
+}
+
+int rt_scene_set_devices(rt_scene* s, const int* devices, int n_devices, int n_ranks) {
+    CHECK_FINISHED(s);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    if (!devices || n_devices < 1 || n_ranks < n_devices || n_ranks % n_devices != 0)
+        return fail(RT_ERR_ARG, "n_devices >= 1 device indices, n_ranks a multiple of n_devices");
+    for (int i = 0; i < n_devices; i++) {
+        if (devices[i] < 0 || devices[i] >= ndev) return fail(RT_ERR_ARG, "device index out of range");
+        for (int j = 0; j < i; j++) if (devices[j] == devices[i]) return fail(RT_ERR_ARG, "a device listed twice");
+    }
+    if (n_ranks > s->h.cam.H) return fail(RT_ERR_ARG, "more ranks than canvas rows");
+    int r;
+    if (s->uploaded && s->device != devices[0]) return fail(RT_ERR_STATE, "devices[0] must be the scene's device");
+    if (!s->uploaded) {
+        const int saved = g_device;
+        g_device = devices[0];
+        r = upload(s);
+        g_device = saved;
+        if (r != RT_OK) return r;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipDeviceSynchronize());
+    free_multi(s);
+    if (n_devices == 1 && n_ranks == 1) return RT_OK;       // back to single-device frames
+    MultiDev* m = new MultiDev;
+    m->devices.assign(devices, devices + n_devices);
+    m->n_ranks = n_ranks; m->per_dev = n_ranks / n_devices;
+    m->W = s->h.cam.W; m->H = s->h.cam.H;
+    m->rows_max = (m->H + n_ranks - 1) / n_ranks;
+    m->reps.push_back(s);
+    m->inst_gen.push_back(s->inst_gen);
+    s->multi = m;
+    return RT_OK;
 }
 
 int rt_timing_collect(rt_scene* s, double* bvh_ms, double* trace_ms, int* n) {

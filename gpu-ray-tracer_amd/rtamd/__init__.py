@@ -36,6 +36,7 @@ SYMBOLS = [
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
     "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_frame_work",
+    "rt_scene_set_devices",
 ]
 
 
@@ -126,6 +127,7 @@ def lib():
     L.rt_device_count.argtypes = [ctypes.POINTER(ip)]
     L.rt_scene_set_frame_slots.argtypes = [vp, ip]
     L.rt_frame_work.argtypes = [vp, ctypes.POINTER(RenderOpts), ctypes.POINTER(Work)]
+    L.rt_scene_set_devices.argtypes = [vp, vp, ip, ip]
     _lib = L
     return L
 
@@ -379,6 +381,12 @@ class Scene:
         w = Work()
         _check(lib().rt_frame_work(self._h, ctypes.byref(o), ctypes.byref(w)))
         return w.as_dict()
+
+    def set_devices(self, devices, n_ranks=None):
+        """Split every whole frame row-cyclically over `devices` from this process (n_ranks
+        slices, RCCL gather to devices[0]; rt_scene_set_devices).  [d], 1 = back to one GPU."""
+        d = np.ascontiguousarray(devices, np.int32)
+        _check(lib().rt_scene_set_devices(self._h, _ptr(d), int(d.size), int(n_ranks or d.size)))
 
     def set_frame_slots(self, n):
         """1 (default) to 4: consecutive frames rotate through n copies of the per-frame

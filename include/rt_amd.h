@@ -168,6 +168,18 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* opts, rt_work* work);
  * outputs.  Images are identical either way.  Waits for the device when changed. */
 int rt_scene_set_frame_slots(rt_scene* s, int n_slots);
 
+/* Multi-GPU frames from one host process (the reference's single-device
+ * update_scene, raytracer.cu:102-120, split over a node's GPUs).  After this call every
+ * whole-frame rt_render / rt_update_scene of the scene renders n_ranks row-cyclic slices
+ * (slice r = rows r, r + n_ranks, ...), ranks [i k, (i+1) k) on devices[i] (k = n_ranks /
+ * n_devices; each device holds a replica of the scene and rebuilds the same BVH), gathers
+ * them to devices[0] with RCCL (ncclGather over ncclCommInitAll communicators) and
+ * un-permutes the rows there: the caller sees one frame, RGBA8 only.  devices[0] is the
+ * scene's device.  n_ranks > n_devices gives several slices per device (on one GPU the
+ * whole sequence runs with a one-rank communicator).  n_devices = n_ranks = 1 returns to
+ * single-device frames.  Camera, instance and environment changes reach every replica. */
+int rt_scene_set_devices(rt_scene* s, const int* devices, int n_devices, int n_ranks);
+
 /* Sum of the event-timed kernel durations of all rt_render calls with timing=1
  * since the last collect (synchronizes those events), then resets. */
 int rt_timing_collect(rt_scene* s, double* bvh_ms_total, double* trace_ms_total, int* n_frames);

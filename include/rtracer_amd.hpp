@@ -194,6 +194,13 @@ namespace gpu {
 inline void update_scene(renv::gpu::Scene* scene, int kernel_dim, bool optimize) {
     rtamd_detail::check(rt_update_scene(scene->handle(), kernel_dim, optimize ? 1 : 0), "update_scene");
 }
+// Build extension: every later update_scene of `scene` renders row-cyclic
+// slices on `devices` (n_ranks slices, default one per device) and gathers them to
+// devices[0] with RCCL; the canvas is the whole frame as before (rt_scene_set_devices).
+inline void use_devices(renv::gpu::Scene* scene, const std::vector<int>& devices, int n_ranks = 0) {
+    rtamd_detail::check(rt_scene_set_devices(scene->handle(), devices.data(), (int)devices.size(),
+                                             n_ranks > 0 ? n_ranks : (int)devices.size()), "use_devices");
+}
 // raytracer.cu:91-100: one-pixel trace with the reference's event log on stdout.
 inline void debug_cast(renv::gpu::Scene* scene, int x, int y) {
     std::vector<char> buf(1 << 16);

@@ -110,3 +110,19 @@ def test_cli_textured_mode(oracle, tmp_path):
     exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
     got = _ppm_rgb(out)
     assert np.abs(got.astype(int) - exp.astype(int)).max() <= 1 and (got != exp).mean() < 1e-3
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 8])
+def test_cli_multi_device_slices(oracle, tmp_path, ranks):
+    """--gpus 1 --ranks R: the reference caller's update_scene through rtracer::gpu::use_devices
+    (rt_scene_set_devices) -- R row-cyclic slices, the RCCL gather (one-rank communicator on a
+    one-GPU box) and the un-permute -- gives the oracle's frame."""
+    out = str(tmp_path / "m.ppm")
+    r = _run([CLI, "-c", scene_path("world8"), "--width", "200", "--height", "121", "--out", out, "--frames", "3",
+              "--gpus", "1", "--ranks", str(ranks)])
+    assert r.returncode == 0, r.stderr
+    assert "slices" in r.stdout
+    o = oracle.render(oracle.load(scene_path("world8"), 200, 121), spp=1, nthreads=8, want=("rgba",))
+    rgba = o["rgba"]
+    exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
+    assert np.array_equal(_ppm_rgb(out), exp)
