@@ -42,7 +42,7 @@ def test_multi_device_frames(gpu, oracle, ranks):
 
 def test_multi_device_rejects(gpu):
     s = gpu.Scene.load_json(scene_path("world8"), 64, 48)
-    for devs, n in (([0, 0], 2), ([0], 0), ([99], 1), ([0], 49)):
+    for devs, n in (([0, 0], 2), ([0], -1), ([99], 1), ([0], 49)):
         with pytest.raises(gpu.RtError) as e:
             s.set_devices(devs, n)
         assert e.value.code == gpu.RT_ERR_ARG, (devs, n)

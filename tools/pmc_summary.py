@@ -5,7 +5,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(root + "/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         if pat in r["Kernel_Name"]:
-            k = r["Kernel_Name"].split("(")[0][-40:]
+            k = r["Kernel_Name"].replace("void (anonymous namespace)::", "").split("((")[0][:60]
             agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     print(k)
