@@ -10,7 +10,7 @@ import sys
 
 
 def short(name):
-    n = name.replace("void (anonymous namespace)::", "")
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
     for k in ("bvh_build_kernel", "sky_kernel", "trace_kernel", "large_"):
         if k in n:
             return n.split("((")[0].split("(")[0]
@@ -24,19 +24,20 @@ def main():
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
         if k:
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), k, r.get("Stream_Id", "0")))
     rows.sort()
     frames, cur = [], {}
-    for s, e, k in rows:                               # a frame = build, sky, trace in dispatch order
+    for s, e, k, sid in rows:                          # a frame = build, sky, trace in order on its stream
         kind = "build" if "bvh_build" in k else "sky" if "sky" in k else "trace" if "trace" in k else None
         if kind == "build":
-            cur = {"build": (s, e)}
-        elif kind and cur is not None:
-            cur[kind] = (s, e)
+            cur[sid] = {"build": (s, e)}
+        elif kind and cur.get(sid) is not None:
+            cur[sid][kind] = (s, e)
             if kind == "trace":
-                cur["trace_name"] = k
-                frames.append(cur)
-                cur = None
+                cur[sid]["trace_name"] = k
+                frames.append(cur[sid])
+                cur[sid] = None
+    frames.sort(key=lambda f: f["trace"][0])
     frames = [f for f in frames if "build" in f][-last:]
     if not frames:
         sys.exit("no frames")
