@@ -18,6 +18,8 @@ Pipelining, two forms:
   streams, see the class.
 The waits are stream dependencies, not host synchronisation.
 """
+import contextlib
+
 import torch
 
 
@@ -100,6 +102,13 @@ class RowCyclicFrame:
         return self.frame
 
 
+class _Done:
+    """A completed event (host-side copies on CPU tensors are synchronous)."""
+
+    def synchronize(self):
+        pass
+
+
 class FramePipeline:
     """`depth` frames in flight (bench.py over RCCL, or one GPU): frame k renders on stream
     k % depth into slice buffer k % depth, with the scene in `depth` frame slots
@@ -125,8 +134,10 @@ class FramePipeline:
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
         self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(D)]
-        self.streams = [torch.cuda.Stream(device=device) for _ in range(D)]
-        self.main = torch.cuda.current_stream(device)
+        # CPU tensors (the gloo tests of the multi-process logic): no streams, no events
+        self.cuda = str(device).startswith("cuda")
+        self.streams = [torch.cuda.Stream(device=device) if self.cuda else None for _ in range(D)]
+        self.main = torch.cuda.current_stream(device) if self.cuda else None
         self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(D)]
                       if (world > 1 and rank == 0) else None)
         self.readback = bool(readback) and (world == 1 or rank == 0)
@@ -135,15 +146,25 @@ class FramePipeline:
                      if (world > 1 and rank == 0) else None)
         self.out = self.outs[0] if self.outs else None
         if self.readback:
-            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=True) for _ in range(D)]
+            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=self.cuda) for _ in range(D)]
             self.host_ev = [None] * D       # D2H copy of the frame last copied into each host buffer
             self.host_no = [-1] * D         # its frame number
-            self.copy_stream = torch.cuda.Stream(device=device) if world > 1 else None
+            self.copy_stream = torch.cuda.Stream(device=device) if (world > 1 and self.cuda) else None
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
         self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
         self.pend_no = [-1] * D         # its frame number
         self.last = -1
+
+    def _on(self, stream):
+        return torch.cuda.stream(stream) if self.cuda else contextlib.nullcontext()
+
+    def _event(self, stream):
+        if not self.cuda:
+            return _Done()
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
 
     @property
     def frame(self):
@@ -156,22 +177,21 @@ class FramePipeline:
         """Frame k (device buffer src, complete on `stream`) -> pinned host buffer s."""
         if self.host_ev[s] is not None:
             self.host_ev[s].synchronize()           # frame k - depth's copy is done (and was read)
-        with torch.cuda.stream(stream):
-            self.host[s].copy_(src, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+        with self._on(stream):
+            self.host[s].copy_(src, non_blocking=self.cuda)
+            ev = self._event(stream)
         self.host_ev[s], self.host_no[s] = ev, k
 
     def _unpermute(self, s):
         if not self.pending[s]:
             return
         self.pending[s] = False
-        with torch.cuda.stream(self.main):
+        with self._on(self.main):
             self.work[s].wait()
             if self.rank == 0:
                 g = self.gbufs[s]
                 out = self.outs[s % len(self.outs)]
-                if self.readback and self.host_ev[s] is not None:
+                if self.readback and self.host_ev[s] is not None and self.cuda:
                     self.main.wait_event(self.host_ev[s])   # frame k - depth's copy has read out
                 if self.H % self.world == 0:
                     out.view(self.rows, self.world, self.W).copy_(g.transpose(0, 1))
@@ -179,25 +199,25 @@ class FramePipeline:
                     for r in range(self.world):
                         out[r::self.world] = g[r][:len(rows_of(r, self.world, self.H))]
                 self.out = out
-                ev = torch.cuda.Event()
-                ev.record(self.main)
+                ev = self._event(self.main)
                 self.unperm[s] = ev
                 if self.readback:
-                    self.copy_stream.wait_event(ev)
+                    if self.cuda:
+                        self.copy_stream.wait_event(ev)
                     self._to_host(s, self.pend_no[s], out, self.copy_stream)
 
     def step(self, k, render):
         """Issue frame k: render(part, stream) enqueues the render of this rank's rows."""
         s = k % self.depth
         st = self.streams[s]
-        with torch.cuda.stream(st):
+        with self._on(st):
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
             render(self.parts[s], st)
             if self.readback and self.world == 1:
                 self._to_host(s, k, self.parts[s], st)
             if self.world > 1:
-                if self.unperm[s] is not None:
+                if self.unperm[s] is not None and self.cuda:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]
                 gl = list(self.gbufs[s].unbind(0)) if self.rank == 0 else None
                 self.work[s] = self.dist.gather(self.parts[s], gl, dst=0, async_op=True)
@@ -221,6 +241,7 @@ class FramePipeline:
         """Complete every issued frame (stream-ordered on the main stream)."""
         for s in range(self.depth):
             self._unpermute(s)
-        for st in self.streams:
-            self.main.wait_stream(st)
+        if self.cuda:
+            for st in self.streams:
+                self.main.wait_stream(st)
         return self.frame

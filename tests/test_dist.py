@@ -70,3 +70,59 @@ def test_rows_partition_covers_frame_once():
             rows = sorted(y for r in range(g) for y in rtdist.rows_of(r, g, h))
             assert rows == list(range(h))
             assert all(len(rtdist.rows_of(r, g, h)) <= rtdist.slice_height(g, h) for r in range(g))
+
+
+def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback):
+    import torch.distributed as dist
+    from oracle_lib import Oracle
+    import rtamd.dist as rtdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc = Oracle()
+        fr = orc.render(orc.load(scene_path(scene), w, h), spp=spp, row0=rank, row_step=world, nthreads=2,
+                        want=("rgba",))
+        mine = torch.from_numpy(np.ascontiguousarray(fr["rgba"].view(np.int32)[list(rtdist.rows_of(rank, world, h))]))
+        pipe = rtdist.FramePipeline(w, h, world, rank, "cpu", dist, depth=depth, readback=readback)
+
+        def render(k):
+            def f(buf, st):
+                buf[:mine.shape[0]] = mine + k               # frame k = image + k
+            return f
+        got = []
+        n = 2 * depth + 2
+        for k in range(n):
+            pipe.step(k, render(k))
+            j = k - depth + 1                                # a host consumer depth - 1 frames behind
+            if readback and rank == 0 and j >= 0:
+                got.append(pipe.host_frame(j).clone().numpy())
+        last = pipe.finish()
+        if rank == 0:
+            if readback:
+                got += [pipe.host_frame(j).clone().numpy() for j in range(n - depth + 1, n)]
+            else:
+                got = [last.clone().numpy()]
+            np.save(out_path, np.stack(got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,h,depth,readback", [(2, 61, 3, False), (3, 60, 4, False), (2, 61, 3, True),
+                                                    (3, 61, 2, True)])
+def test_frame_pipeline_gather_across_processes(oracle, tmp_path, world, h, depth, readback):
+    """rtamd.dist.FramePipeline (bench.py's default N > 1 path) across processes: frames in
+    flight, asynchronous gathers into per-slot buffers, the un-permute one frame later, and
+    (readback) every frame's host copy -- the frame k that rank 0 reads is image + k."""
+    scene, w, spp = "world8_stress", 96, 2
+    out_path = str(tmp_path / "frames.npy")
+    mp.spawn(_pipe_main, args=(world, _free_port(), scene, w, h, spp, out_path, depth, readback), nprocs=world,
+             join=True)
+    full = oracle.render(oracle.load(scene_path(scene), w, h), spp=spp, nthreads=4, want=("rgba",))["rgba"].view(np.int32)
+    got = np.load(out_path)
+    n = 2 * depth + 2
+    if readback:
+        assert got.shape[0] == n
+        for k in range(n):
+            assert np.array_equal(got[k], full + k), k
+    else:
+        assert np.array_equal(got[0], full + n - 1)
