@@ -585,6 +585,10 @@ BVH build_bvh(const orc_scene& s, bool cpu_flavour) {
 // Intersection (scene.cu:27-73, hitable.cu:7-38, trimesh.cu:11-68)
 // ----------------------------------------------------------------------------
 struct Isect { float time; V3 norm; float u, v; int mat; int inst, tri; };
+// debug_cast's event log (raytracer.cu:91-100: env.set_debug_mode(true) around one ray; the
+// printf sites scene.cu:107-108, 134-135, 152-153 and light.cu:38-39), NULL otherwise
+thread_local std::string* g_dbg = nullptr;
+inline void dbg_event(const char* e) { if (g_dbg) { *g_dbg += e; *g_dbg += '\n'; } }
 struct Counters { uint64_t rays = 0, nodes = 0, leaves = 0, tris = 0; };
 
 struct Ctx {
@@ -686,6 +690,7 @@ V4 attenuate(const Ctx& x, const Light& L, const Ray& to_light, float max_t) {  
     Ray cur = make_ray(ray_at(to_light, THRESH), to_light.d);
     for (;;) {
         Isect si; si.time = INFINITY; si.mat = -1; si.inst = -1; si.tri = -1; si.norm = v3(0, 0, 0);
+        dbg_event("shooting shadow ray");                                    // light.cu:38-39
         if (cast_ray(x, cur, si)) {
             if (si.time > max_t) return rv;
             const Material& m = x.s->mats[si.mat];
@@ -756,6 +761,7 @@ V4 propagate_gpu(const Ctx& x, const Ray& r, Isect& is) {                   // s
         switch (top.type) {
             case NORMAL: {
                 is.time = INFINITY;
+                dbg_event("shooting a ray");                                     // scene.cu:107-108
                 if (cast_ray(x, top.ray, is)) {
                     if (top.depth > 0) {
                         if (top.in_obj) top.atten = mul4(top.atten, trans_atten(s.mats[is.mat], is.time));
@@ -776,6 +782,7 @@ V4 propagate_gpu(const Ctx& x, const Ray& r, Isect& is) {                   // s
                 const Material& m = s.mats[is.mat];
                 top.type = REFRACT;
                 if (reflective(m)) {
+                    dbg_event("preparing to shoot a reflection ray");            // scene.cu:134-135
                     top_i++;
                     RayFrame& nt = frames[top_i];
                     nt.type = NORMAL; nt.last_mat = top.last_mat; nt.in_obj = top.in_obj;
@@ -788,6 +795,7 @@ V4 propagate_gpu(const Ctx& x, const Ray& r, Isect& is) {                   // s
             case REFRACT: {
                 const Material& m = s.mats[is.mat];
                 if (refractive(m)) {
+                    dbg_event("preparing to shoot a refraction ray");            // scene.cu:152-153
                     top.type = NORMAL;
                     float n1, n2; bool tir;
                     if (top.in_obj) { n1 = s.mats[top.last_mat].eta; n2 = 1.0f; }
@@ -1074,6 +1082,26 @@ int orc_scene_camera(const orc_scene* s, float* c, float* env) {
     memcpy(c, v, 21 * sizeof(float));
     float e[7] = {s->dist_atten.x, s->dist_atten.y, s->dist_atten.z, s->ambience.x, s->ambience.y, s->ambience.z, s->ambience.w};
     memcpy(env, e, sizeof e);
+    return 0;
+}
+
+// debug_cast (raytracer.cu:45-52, 91-100): one ray through pixel (x, y) -- Camera::at with
+// the integer pixel, propagate_ray with the debug printfs on -- its event log into buf.
+int orc_debug_cast(const orc_scene* s, int x, int y, int use_bvh, char* buf, int64_t cap) {
+    if (!s || s->building || x < 0 || y < 0 || x >= s->W || y >= s->H || !buf || cap <= 0) return -1;
+    BVH bvh = build_bvh(*s, false);
+    Counters c;
+    Ctx cx{s, &bvh, use_bvh != 0, false, &c};
+    CamBasis cb = cam_basis(s->cam);
+    Ray r = cam_at(s->cam, cb, (float)x, (float)y);
+    Isect is; is.time = INFINITY; is.mat = -1; is.inst = -1; is.tri = -1; is.norm = v3(0, 0, 0);
+    std::string log;
+    g_dbg = &log;
+    (void)propagate_gpu(cx, r, is);
+    g_dbg = nullptr;
+    const size_t m = std::min(log.size(), (size_t)cap - 1);
+    memcpy(buf, log.data(), m);
+    buf[m] = 0;
     return 0;
 }
 

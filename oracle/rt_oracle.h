@@ -90,6 +90,11 @@ int orc_render(const orc_scene* s, int semantics, int use_bvh, int spp,
                uint32_t* rgba, float* radiance, int32_t* hit_inst, int32_t* hit_tri,
                uint64_t* stats);
 
+/* debug_cast (raytracer.cu:91-100): the event log ("shooting a ray", "preparing to shoot a
+ * reflection ray", "preparing to shoot a refraction ray", "shooting shadow ray", one per line,
+ * scene.cu:107-153 / light.cu:38-39) of pixel (x, y)'s ray, into buf (NUL-terminated). */
+int orc_debug_cast(const orc_scene* s, int x, int y, int use_bvh, char* buf, int64_t cap);
+
 /* Sub-pixel sample offset table (build-defined spp extension). */
 void orc_spp_offset(int k, float* dx, float* dy);
 

@@ -57,6 +57,7 @@ class Oracle:
         L.orc_set_camera.argtypes = [vp, vp, vp]
         L.orc_set_trans.argtypes = [vp, ctypes.c_int, vp, vp]
         L.orc_set_env.argtypes = [vp, vp, vp, ctypes.c_int]
+        L.orc_debug_cast.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int64]
         self.L = L
 
     # -- scenes ---------------------------------------------------------------
@@ -215,6 +216,12 @@ class OracleScene:
         a = [_fa(cam_pos, 3), _fa(cam_quat, 4), _fa(dist_atten, 3), _fa(ambience, 4)]
         assert self.orc.L.orc_builder_finish(self.h, width, height, fov, unit, *[_vp(x) for x in a], depth) == 0
         self._counts()
+
+    def debug_cast(self, x, y, use_bvh=True):
+        """debug_cast's event log of pixel (x, y) (raytracer.cu:91-100), one event per line."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        assert self.orc.L.orc_debug_cast(self.h, x, y, int(use_bvh), buf, len(buf)) == 0
+        return buf.value.decode().splitlines()
 
     # -- poses / environment (Entity setters, entity.h:49-74) -------------------
     def set_camera(self, pos=None, quat=None):

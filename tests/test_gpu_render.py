@@ -124,14 +124,36 @@ def test_camera_move_rerender(gpu, oracle):
     assert not np.array_equal(fr["rgba"], first)
 
 
-def test_debug_cast_log(gpu):
+def test_debug_cast_log(gpu, oracle):
+    """debug_cast's whole event log (raytracer.cu:91-100; printf sites scene.cu:107-153 and
+    light.cu:38-39, in order) equals the oracle's for lit, mirror, sky and -- world1 seen from
+    a moved camera -- refraction pixels (shadow segments through the Kt cube)."""
     s = gpu.Scene.load_json(scene_path("world8_stress"), 320, 240)
+    o = oracle.load(scene_path("world8_stress"), 320, 240)
     fr = s.render(want=("hit_inst",))
     ys, xs = np.nonzero(fr["hit_inst"] >= 0)
     log = s.debug_cast(int(xs[0]), int(ys[0]))
     assert log[0] == "shooting a ray" and "shooting shadow ray" in log
     ys, xs = np.nonzero(fr["hit_inst"] < 0)
     assert s.debug_cast(int(xs[0]), int(ys[0])) == ["shooting a ray"]
+    kinds = set()
+    for x in range(3, 320, 17):
+        for y in range(5, 240, 13):
+            g = s.debug_cast(x, y)
+            assert g == o.debug_cast(x, y), (x, y)
+            kinds |= set(g)
+    assert "preparing to shoot a reflection ray" in kinds
+    w = gpu.Scene.load_json(scene_path("world1"), 64, 48)
+    ow = oracle.load(scene_path("world1"), 64, 48)
+    w.set_camera([0.5, 2.0, -3.0], [0.2, 0.0, 0.0, 0.98])
+    mirror_camera(w, ow)
+    refr = 0
+    for x in range(0, 64, 3):
+        for y in range(0, 48, 3):
+            g = w.debug_cast(x, y)
+            assert g == ow.debug_cast(x, y), (x, y)
+            refr += "preparing to shoot a refraction ray" in g
+    assert refr >= 10
 
 
 def test_empty_scene_renders_black(gpu, tmp_path):
