@@ -862,10 +862,15 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // registers free (instead of the allocator spilling to scratch, whose working set is
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
+// NS = 0 kernels run only scenes without a refractive material (launch_trace): there a shadow
+// ray's light is never attenuated (rv = the light's colour) and the direction to the light is
+// recomputed after the query from the same operands, so they park 7 fields fewer.
 constexpr int PARK_FIELDS = 25;
+__host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 18 : PARK_FIELDS; }
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
+    constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
     KTP& P0 = kparams();
     Frame cur;
     SavedFrame stk[NS > 0 ? NS : 1];
@@ -971,7 +976,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     cur.depth = cur.depth - 1;
                     cur.ray = make_ray(hp, reflect(cur.ray.d, normalized(is_norm)));
                 }
-            } else if (m.refractive) {                            // F_REFRACT (scene.cu:149-184)
+            } else if (!OPQ && m.refractive) {                    // F_REFRACT (scene.cu:149-184)
                 dbg(P, me, 3);
                 cur.type = F_NORMAL;
                 float n1, n2;
@@ -1005,8 +1010,10 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             put(cur.atten.x); put(cur.atten.y); put(cur.atten.z); put(cur.atten.w);
             put(acc.x); put(acc.y); put(acc.z); put(acc.w);
             put(summed.x); put(summed.y); put(summed.z); put(summed.w);
-            put(rv.x); put(rv.y); put(rv.z); put(rv.w);
-            put(dtl.x); put(dtl.y); put(dtl.z);
+            if (!OPQ) {
+                put(rv.x); put(rv.y); put(rv.z); put(rv.w);
+                put(dtl.x); put(dtl.y); put(dtl.z);
+            }
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1023,8 +1030,10 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             cur.atten.x = get(); cur.atten.y = get(); cur.atten.z = get(); cur.atten.w = get();
             acc.x = get(); acc.y = get(); acc.z = get(); acc.w = get();
             summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
-            rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get();
-            dtl.x = get(); dtl.y = get(); dtl.z = get();
+            if (!OPQ) {
+                rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get();
+                dtl.x = get(); dtl.y = get(); dtl.z = get();
+            }
         }
         unsigned long long c1 = 0;
         if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
@@ -1052,7 +1061,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             if (TEX) is_kd = hit_kd(P, bv, b, hmat);
             fl &= ~4;                                              // hit point / normal = at(ray, is_time), is_norm
             if (cur.depth > 0) {                                   // scene.cu:109-121
-                if (cur.in_obj) {
+                if (!OPQ && cur.in_obj) {
                     const V4 kt = bv.mats[is_mat].Kt;               // trans_atten (scene.cu:14-22): time^Kt
                     cur.atten = cur.atten * v4(pow_fast(is_time, kt.x), pow_fast(is_time, kt.y),
                                                pow_fast(is_time, kt.z), pow_fast(is_time, kt.w));
@@ -1070,10 +1079,13 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         }
         // ST_WAIT_SHADOW: one shadow segment (light.cu:35-58)
         bool light_done = true;
+        if (OPQ && PARK) {                                     // not parked: the light's own colour
+            rv = bv.lights[li].col;
+        }
         V4 att = rv;
         if (hit && !(b.time > max_t)) {
             const DMat& m = bv.mats[hmat];
-            if (!m.refractive) {
+            if (OPQ || !m.refractive) {
                 att = v4(0, 0, 0, 0);
             } else {
                 if (dot(hn, q.d) > 0) {                            // calc_shadow_atten (light.cu:18-25)
@@ -1087,6 +1099,10 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             }
         }
         if (light_done) {
+            if (OPQ && PARK) {                                 // not parked: the same operations as ST_LIGHT
+                const DLight L = bv.lights[li];
+                dtl = L.type == 0 ? normalized(L.v - at(cur.ray, is_time)) : neg(L.v);
+            }
             const V4 inc = (bv.lights[li].type == 0) ? da * att : att;  // PointLight: dist_atten * attenuate()
             const DMat& mm = bv.mats[is_mat];
             summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
@@ -2446,7 +2462,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     // suspended frames needed (<= MAX_FRAMES - 1); none without a refractive material, where a
     // reflection child replaces its parent (trace_sample, F_REFLECT)
-    const int ns = opaque_scene(s) ? 0 : h.depth;
+    // (NS = 0 kernels assume that: a depth-0 scene with refraction takes the NS = 2 bucket)
+    const int ns = opaque_scene(s) ? 0 : std::max(h.depth, 1);
     const void* fn;
     const int mode = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
     constexpr int NG = MAX_FRAMES - 1;                     // generic frame-stack depth
@@ -2460,7 +2477,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
          (const void*)trace_kernel<NG, false, 10>, (const void*)trace_kernel<NG, false, 11>},
         {(const void*)trace_kernel<NG, true, 8>, (const void*)trace_kernel<NG, true, 9>,
          (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
-    const size_t park_bytes = (size_t)PARK_FIELDS * 4 * TRACE_BLOCK_P;
+    const size_t park_bytes = (size_t)park_fields(ns <= 0 ? 0 : 2) * 4 * TRACE_BLOCK_P;
     const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
     const bool shade = park && ft && S.tri_ax && !prof &&
