@@ -867,7 +867,7 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // recomputed after the query from the same operands, so they park 7 fields fewer.
 constexpr int PARK_FIELDS = 25;
 __host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 18 : PARK_FIELDS; }
-template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false, int BP = TRACE_BLOCK_P>
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
     constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
@@ -1005,7 +1005,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         if (PARK) {
             float* pk = park;
             int f = 0;
-            auto put = [&](float v) { pk[(f++) * BP] = v; };
+            auto put = [&](float v) { pk[(f++) * TRACE_BLOCK_P] = v; };
             put(cur.ray.o.x); put(cur.ray.o.y); put(cur.ray.o.z); put(cur.ray.d.x); put(cur.ray.d.y); put(cur.ray.d.z);
             put(cur.atten.x); put(cur.atten.y); put(cur.atten.z); put(cur.atten.w);
             put(acc.x); put(acc.y); put(acc.z); put(acc.w);
@@ -1024,7 +1024,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             asm volatile("" ::: "memory");
             const float* pk = park;
             int f = 0;
-            auto get = [&]() { return pk[(f++) * BP]; };
+            auto get = [&]() { return pk[(f++) * TRACE_BLOCK_P]; };
             cur.ray.o.x = get(); cur.ray.o.y = get(); cur.ray.o.z = get();
             cur.ray.d.x = get(); cur.ray.d.y = get(); cur.ray.d.z = get();
             cur.atten.x = get(); cur.atten.y = get(); cur.atten.z = get(); cur.atten.w = get();
@@ -1120,10 +1120,9 @@ __host__ __device__ inline size_t shade_bytes(const SceneView& S) {
     return a16(sizeof(DMat) * (size_t)S.n_mats) + a16(sizeof(DLight) * (size_t)S.n_lights) +
            a16(sizeof(DTri) * (size_t)S.n_tris) + a16(sizeof(DMesh) * (size_t)S.n_meshes);
 }
-// half: the 512-thread blocks (M_HALF) keep the instance records in global memory
-__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false, bool half = false) {
+__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false) {
     const size_t sh = shade ? shade_bytes(S) : 0;
-    if (ft) return 64 * (size_t)(S.n_real - 1) + (half ? 0 : 16 * (size_t)S.n_inst) + sh;
+    if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
     return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
 }
 // word copy of n records of T into LDS at `dst` (block-cooperative)
@@ -1138,7 +1137,7 @@ template <class T> __device__ __forceinline__ const T* stage_words(unsigned char
 
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
-template <bool LDS, bool FT = false, bool SHADE = false, bool HALF = false>
+template <bool LDS, bool FT = false, bool SHADE = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
     bv.fnode = S.fnode;
@@ -1157,10 +1156,9 @@ __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* 
         float4* fn = reinterpret_cast<float4*>(smem);
         float4* in = fn + nf;
         for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = src[i];
-        if (!HALF) for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
         __syncthreads();
-        bv.fnode = fn;
-        if (!HALF) bv.inst = in;
+        bv.fnode = fn; bv.inst = in;
     } else if (LDS) {
         const int n3 = 3 * S.n_leaf;
         float4* np = reinterpret_cast<float4*>(smem);
@@ -1195,28 +1193,21 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
 // MODE bit 6 (PROF): profiling variant of the fast kernel -- wave-level step counts and
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
-// MODE bit 8 (HALF): 512-thread blocks, two per CU (the scene image without the instance records
-// and the parking area of 512 lanes fit twice in the LDS): a block whose last waves run a frame's
-// longest groups holds half a CU, not a whole one.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128,
-              M_HALF = 256;
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128;
 template <int NS, bool LDS, int MODE>
-__global__ __launch_bounds__((MODE & M_HALF) ? TRACE_BLOCK_P / 2 : TRACE_BLOCK_P) __attribute__((amdgpu_waves_per_eu(4)))
-void trace_kernel(TraceParams P_arg, SceneView S) {
+__global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     (void)P_arg;                                               // read in place: kparams()
     KTP& P = kparams();
     constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
     constexpr bool SHADE = (MODE & M_SHADE) != 0;
-    constexpr bool HALF = (MODE & M_HALF) != 0;
-    constexpr int BP = HALF ? TRACE_BLOCK_P / 2 : TRACE_BLOCK_P;
-    const BvhRefs bv = stage_bvh<LDS, FT, SHADE, HALF>(S, smem);
+    const BvhRefs bv = stage_bvh<LDS, FT, SHADE>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
-    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE, HALF)) + threadIdx.x : nullptr;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
@@ -1348,7 +1339,7 @@ void trace_kernel(TraceParams P_arg, SceneView S) {
                 break;                                         // sum_c = sum_r = 0
             }
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF, BP>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
@@ -2491,16 +2482,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
     const bool shade = park && ft && S.tri_ax && !prof &&
                        lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    // Half-size blocks (M_HALF, two per CU): opaque-scene fast frames whose tree image and the
-    // parking of 512 lanes fit in half the LDS.  RT_HALF_BLOCKS=0/1 overrides (A/B).
-    static const int half_env = [] { const char* e = getenv("RT_HALF_BLOCKS"); return e ? atoi(e) : -1; }();
-    const size_t half_lds = lds_bytes(S, true, false, true) + (size_t)park_fields(0) * 4 * (TRACE_BLOCK_P / 2);
-    const bool half = ft && park && S.tri_ax && !prof && ns <= 0 && half_lds <= 80 * 1024 && half_env == 1;
-    int bp = TRACE_BLOCK_P;
-    if (half) {
-        fn = (const void*)trace_kernel<0, true, M_PARK | M_FT | M_AXIS | M_HALF>;
-        bp = TRACE_BLOCK_P / 2;
-    } else if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
+    if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
         constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
         fn = S.tri_ax ? (ns <= 2 ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<NG, true, TA>)
                       : (ns <= 2 ? (const void*)trace_kernel<2, true, TF> : (const void*)trace_kernel<NG, true, TF>);
@@ -2530,14 +2512,14 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = half ? half_lds : (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0);
+    const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, bp, shm) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
     const int waves_needed = P.n_groups;
-    int blocks = std::min(s->n_cu * per_cu, (waves_needed + bp / 64 - 1) / (bp / 64));
+    int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
-    P.heavy_cap = std::max(2 * blocks * (bp / 64), P.n_groups / 4);   // a bound, not a target
+    P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     // longest-first history (fast frames): valid while the launch layout is unchanged
     // Only where a wave runs few groups (1080p 8-way row slices: ~8 per wave): with more (63
     // for a whole 1080p frame, 16 for a 4-way slice) the dynamic queues already balance the
@@ -2545,7 +2527,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // (measured, four frames in flight, ms per frame with / without: whole frame 0.919 / 0.914,
     // 4-way 0.360 / 0.360, 8-way 0.179-0.186 / 0.200-0.204; profiles/r02/hist_policy.log).
     P.hist = 0;
-    const long long waves = (long long)blocks * (bp / 64);
+    const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
     if (!want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
         const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
         int r;
@@ -2583,7 +2565,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
     }
     void* args[] = {&P, &S};
-    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(bp), args, shm, st, sky ? nullptr : e0, e1, 0));
+    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
