@@ -760,7 +760,8 @@ struct TraceParams {
     // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
     const int* live; int live_cap;
     int tpc;                  // work indices per ticket (normal queues)
-    int unlit_skip;           // fast frames: no shadow segments for a light whose phong factor is zero
+    int unlit_skip;           // fast frames: no shadow segments for a light whose phong factor is zero (1),
+                              // and no phong term for it either (2)
 };
 
 // The launch's TraceParams read in place from the kernel-argument segment (constant address
@@ -1040,7 +1041,9 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         if (!need) continue;
         int hmat = 0;
         V3 hn = v3(0, 0, 0);
-        if (hit) hn = hit_normal(S, bv, b, hmat);
+        // (opaque scenes: a shadow segment needs neither the normal nor the material -- any hit
+        // before the light is opaque, light.cu:44-46)
+        if (hit && (!OPQ || st == ST_WAIT_NORMAL)) hn = hit_normal(S, bv, b, hmat);
         if (st == ST_WAIT_NORMAL) {
             if (fl & 1) {
                 fl &= ~1;
@@ -1099,13 +1102,18 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             }
         }
         if (light_done) {
-            if (OPQ && PARK) {                                 // not parked: the same operations as ST_LIGHT
-                const DLight L = bv.lights[li];
-                dtl = L.type == 0 ? normalized(L.v - at(cur.ray, is_time)) : neg(L.v);
+            // An unlit light's term is its factor's signed zeros times the light: adding it leaves
+            // `summed` as it is unless `summed` is -0, which the host rules out (unlit_skip = 2:
+            // no material's Ke + Ka * ambience has a -0 channel, and x + y is -0 only for two -0).
+            if (!(max_t == -INFINITY && kparams().unlit_skip == 2)) {
+                if (OPQ && PARK) {                             // not parked: the same operations as ST_LIGHT
+                    const DLight L = bv.lights[li];
+                    dtl = L.type == 0 ? normalized(L.v - at(cur.ray, is_time)) : neg(L.v);
+                }
+                const V4 inc = (bv.lights[li].type == 0) ? da * att : att;  // PointLight: dist_atten * attenuate()
+                const DMat& mm = bv.mats[is_mat];
+                summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
             }
-            const V4 inc = (bv.lights[li].type == 0) ? da * att : att;  // PointLight: dist_atten * attenuate()
-            const DMat& mm = bv.mats[is_mat];
-            summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
             li++;
             st = ST_LIGHT;
         }
@@ -2451,7 +2459,12 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         for (const DMat& m : h.d_mats)
             ok = ok && pos0(m.Kt.x) && pos0(m.Kt.y) && pos0(m.Kt.z) && pos0(m.Kt.w) && m.Kt.x <= 1.0f && m.Kt.y <= 1.0f &&
                  m.Kt.z <= 1.0f && m.Kt.w <= 1.0f;
-        P.unlit_skip = ok ? 1 : 0;
+        bool start_ok = true;                                  // no -0 channel in Ke + Ka * ambience (org_light)
+        for (const DMat& m : h.d_mats) {
+            const V4 o = m.Ke + m.Ka * h.ambience;
+            for (float v : {o.x, o.y, o.z, o.w}) start_ok = start_ok && !(v == 0.0f && std::signbit(v));
+        }
+        P.unlit_skip = ok ? (start_ok ? 2 : 1) : 0;
     }
     P.occl_exit = (opaque_scene(s) && (occl_force == 1 || (occl_force < 0 && !want_stats))) ? 1 : 0;
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, WORK_INTS * sizeof(int), st));
