@@ -36,45 +36,12 @@ RT_HD V3 neg(V3 v) { return (-1.0f) * v; }                           // (T)-1 * 
 RT_HD float dot(V3 a, V3 b) {                                       // linear.h:197-205: 0 + x*x + ...
     float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s;
 }
-// Correctly rounded sqrt and reciprocal.  The host uses the IEEE operations; the device
-// uses shorter exact sequences inside a safe range and the compiler's general ones outside:
-//  * rcp_cr(x), 2^-125 <= |x| <= 2^125: v_rcp_f32 (<= 1 ulp) and two Newton steps with
-//    FMA (e = 1 - x r is exact once r is faithful, Markstein);
-//  * sqrt_cr(x), 2^-100 <= x <= 2^100: v_sqrt_f32 and the +-1 ulp residual selection the
-//    compiler itself emits, without its subnormal scaling and 0/inf/NaN guards.
-// Both are checked bit for bit against IEEE on the device over every significand of
-// two binades and 4M random inputs (tests/test_gpu_kat.py::test_device_cr_rcp_sqrt).
-// Off by default (EXTRA=-DRT_SHORT_CR=1 turns them on): measured no faster on the bench
-// frame (2.72 vs 2.69 ms) while growing the code object by a quarter.
-#ifndef RT_SHORT_CR
-#define RT_SHORT_CR 0
-#endif
-RT_HD float rcp_cr(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SHORT_CR
-    const float ax = fabsf(x);
-    if (__builtin_expect(ax >= 0x1p-125f && ax <= 0x1p125f, 1)) {
-        float r = __builtin_amdgcn_rcpf(x);
-        float e = __builtin_fmaf(-x, r, 1.0f);
-        r = __builtin_fmaf(e, r, r);
-        e = __builtin_fmaf(-x, r, 1.0f);
-        return __builtin_fmaf(e, r, r);
-    }
-#endif
-    return 1.0f / x;
-}
-RT_HD float sqrt_cr(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SHORT_CR
-    if (__builtin_expect(x >= 0x1p-100f && x <= 0x1p100f, 1)) {
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const float sd = __int_as_float(__float_as_int(s) - 1), su = __int_as_float(__float_as_int(s) + 1);
-        float r = s;
-        if (__builtin_fmaf(-sd, s, x) <= 0.0f) r = sd;
-        if (__builtin_fmaf(-su, s, x) > 0.0f) r = su;
-        return r;
-    }
-#endif
-    return sqrtf(x);
-}
+// Correctly rounded sqrt and reciprocal (IEEE, the HIP defaults on gfx950: the compiler's
+// exact sequences).  A shorter exact device form (v_rcp / v_sqrt with Newton and residual
+// corrections) measured no faster while growing the code by a quarter and was
+// removed; tests/test_gpu_kat.py still checks these bit for bit against IEEE.
+RT_HD float rcp_cr(float x) { return 1.0f / x; }
+RT_HD float sqrt_cr(float x) { return sqrtf(x); }
 
 RT_HD float len(V3 v) { return sqrt_cr(dot(v, v)); }
 RT_HD V3 normalized(V3 v) {                                         // linear.h:159-167

@@ -162,8 +162,8 @@ def test_packed_pair_box_test_equals_exact(gpu, oracle):
 
 
 def test_device_cr_rcp_sqrt(gpu):
-    """rt_math.h rcp_cr/sqrt_cr (the device's short correctly rounded reciprocal and sqrt)
-    against IEEE float32 (numpy), bit for bit: every significand of the binades [1, 4)
+    """rt_math.h rcp_cr/sqrt_cr (the device's correctly rounded reciprocal and sqrt, the
+    compiler's sequences) against IEEE float32 (numpy), bit for bit: every significand of the binades [1, 4)
     (rounding depends only on the significand, and for sqrt on the exponent's parity),
     both signs for rcp, plus 4M random bit patterns over the whole float range (the
     out-of-range inputs take the compiler's general sequences)."""
