@@ -705,9 +705,7 @@ __device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_
     V4 specular = pow_fast(max_std(rd, 0.0f), m.alpha) * m.Ks;
     return diffuse + specular;
 }
-__device__ __forceinline__ V4 phong(const DMat& m, V4 kd, V3 nrm, V4 incoming, V3 ray_dir, V3 to_light) {
-    return phong_factor(m, kd, nrm, ray_dir, to_light) * incoming;
-}
+// phong(m, kd, nrm, incoming, ...) = phong_factor(m, kd, nrm, ...) * incoming (trace_sample's light step)
 
 // RayFrame (scene.cu:81-90).  The top frame's hit point and normal are not kept in
 // registers: while the frame is being lit they equal at(ray, is_time) and is_norm
@@ -863,11 +861,13 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // registers free (instead of the allocator spilling to scratch, whose working set is
 // larger than L2: measured ~0.9 GB of write-back per frame).  The memory clobbers
 // stop the compiler from forwarding the stored values and keeping them live.
-// NS = 0 kernels run only scenes without a refractive material (launch_trace): there a shadow
-// ray's light is never attenuated (rv = the light's colour) and the direction to the light is
-// recomputed after the query from the same operands, so they park 7 fields fewer.
-constexpr int PARK_FIELDS = 25;
-__host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 18 : PARK_FIELDS; }
+// The light's phong factor (phong.cu:14-53 without the incoming light) is formed once, when the
+// shadow query is set up, and parked: the light's term after the query is factor x incoming,
+// the same operations in the same order as the reference's phong.  NS = 0 kernels run only scenes without a
+// refractive material (launch_trace): there a shadow ray's light is never attenuated (rv = the
+// light's colour, reloaded after the query), so they park 4 fields fewer.
+constexpr int PARK_FIELDS = 26;
+__host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 22 : PARK_FIELDS; }
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
@@ -886,7 +886,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
     V4 is_kd = v4(0, 0, 0, 0);                                  // textured mode: the hit's diffuse colour
     int li = 0;
     V4 summed = v4(0, 0, 0, 0), rv = v4(0, 0, 0, 0);
-    V3 dtl = v3(0, 0, 0);
+    V4 fct = v4(0, 0, 0, 0);                                    // the light's phong factor
     float da = 1.0f, max_t = 0.0f;
     Ray q = r0;
     if (valid) {
@@ -910,6 +910,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     const DLight L = bv.lights[li];
                     const V3 hpos = at(cur.ray, is_time);          // org_ray.at(isect.time) (phong.cu:48)
                     Ray to;
+                    V3 dtl;
                     if (L.type == 0) {                             // PointLight::shine (light.cu:63-70)
                         V3 disp = L.v - hpos;
                         float dist = len(disp);
@@ -933,11 +934,10 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     // The lane still takes the wait-for-shadow step, with no query (max_t = -inf
                     // marks it): no hit, so the light's term is phong's with the unshadowed
                     // light, the same signed zeros.
-                    if (P.unlit_skip) {
-                        const DMat& mm = bv.mats[is_mat];
-                        const V4 f = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl);
-                        if (f.x == 0.0f && f.y == 0.0f && f.z == 0.0f && f.w == 0.0f) max_t = -INFINITY;
-                    }
+                    const DMat& mm = bv.mats[is_mat];
+                    fct = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl);
+                    if (P.unlit_skip && fct.x == 0.0f && fct.y == 0.0f && fct.z == 0.0f && fct.w == 0.0f)
+                        max_t = -INFINITY;
                     q = make_ray(at(to, THRESH), to.d);
                     dbg(P, me, 4);
                     st = ST_WAIT_SHADOW;
@@ -1011,10 +1011,8 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             put(cur.atten.x); put(cur.atten.y); put(cur.atten.z); put(cur.atten.w);
             put(acc.x); put(acc.y); put(acc.z); put(acc.w);
             put(summed.x); put(summed.y); put(summed.z); put(summed.w);
-            if (!OPQ) {
-                put(rv.x); put(rv.y); put(rv.z); put(rv.w);
-                put(dtl.x); put(dtl.y); put(dtl.z);
-            }
+            put(fct.x); put(fct.y); put(fct.z); put(fct.w);
+            if (!OPQ) { put(rv.x); put(rv.y); put(rv.z); put(rv.w); }
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
@@ -1031,10 +1029,8 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             cur.atten.x = get(); cur.atten.y = get(); cur.atten.z = get(); cur.atten.w = get();
             acc.x = get(); acc.y = get(); acc.z = get(); acc.w = get();
             summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
-            if (!OPQ) {
-                rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get();
-                dtl.x = get(); dtl.y = get(); dtl.z = get();
-            }
+            fct.x = get(); fct.y = get(); fct.z = get(); fct.w = get();
+            if (!OPQ) { rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get(); }
         }
         unsigned long long c1 = 0;
         if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
@@ -1106,13 +1102,8 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             // `summed` as it is unless `summed` is -0, which the host rules out (unlit_skip = 2:
             // no material's Ke + Ka * ambience has a -0 channel, and x + y is -0 only for two -0).
             if (!(max_t == -INFINITY && kparams().unlit_skip == 2)) {
-                if (OPQ && PARK) {                             // not parked: the same operations as ST_LIGHT
-                    const DLight L = bv.lights[li];
-                    dtl = L.type == 0 ? normalized(L.v - at(cur.ray, is_time)) : neg(L.v);
-                }
                 const V4 inc = (bv.lights[li].type == 0) ? da * att : att;  // PointLight: dist_atten * attenuate()
-                const DMat& mm = bv.mats[is_mat];
-                summed = summed + phong(mm, TEX ? is_kd : mm.Kd, is_norm, inc, cur.ray.d, dtl);
+                summed = summed + fct * inc;                   // phong(): factor x incoming (phong.cu:50-52)
             }
             li++;
             st = ST_LIGHT;
