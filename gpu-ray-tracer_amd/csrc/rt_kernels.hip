@@ -697,10 +697,13 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
 // ---------------------------------------------------------------------------
 // kd: the material's Kd (the reference), or the atlas texel in the textured mode
 // diffuse + specular: phong's factor of the incoming light
-__device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_dir, V3 to_light) {
+// tl_len = len(to_light), tl_neg_unit = normalized(neg(to_light)) (the shadow ray's direction
+// negated: the light step has them)
+__device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_dir, V3 to_light, float tl_len,
+                                           V3 tl_neg_unit) {
     float nd = max_std(dot(to_light, nrm), 0.0f);
     V4 diffuse = nd * kd;
-    V3 reflected = reflect(neg(to_light), nrm);
+    V3 reflected = reflect_pre(tl_len, tl_neg_unit, normalized(nrm));   // reflect(neg(to_light), nrm)
     float rd = dot(neg(reflected), ray_dir);
     V4 specular = pow_fast(max_std(rd, 0.0f), m.alpha) * m.Ks;
     return diffuse + specular;
@@ -909,7 +912,6 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                 if (li < S.n_lights) {
                     const DLight L = bv.lights[li];
                     const V3 hpos = at(cur.ray, is_time);          // org_ray.at(isect.time) (phong.cu:48)
-                    Ray to;
                     V3 dtl;
                     if (L.type == 0) {                             // PointLight::shine (light.cu:63-70)
                         V3 disp = L.v - hpos;
@@ -917,13 +919,20 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                         float quad = P.dist_atten.x + P.dist_atten.y * dist + P.dist_atten.z * dist * dist;
                         da = quad < 1.0f ? 1.0f : 1.0f / quad;
                         dtl = normalized(disp);
-                        to = make_ray(hpos, dtl);
                         max_t = dist;
                     } else {                                       // DirLight::shine (light.cu:72-77)
                         dtl = neg(L.v);
-                        to = make_ray(hpos, dtl);
                         max_t = INFINITY;
                     }
+                    // to = make_ray(hpos, dtl): normalized(dtl) formed here once; phong's
+                    // reflect(neg(dtl), n) takes |neg(dtl)| = |dtl| (the same squares) and
+                    // normalized(neg(dtl)) = neg(normalized(dtl)) (the same magnitudes, RNE is
+                    // sign-symmetric; +0s below THRESH in both)
+                    const float tl = len(dtl);
+                    const bool tl_ok = tl > THRESH;
+                    const float tr = rcp_cr(tl);
+                    const Ray to{hpos, tl_ok ? tr * dtl : v3(0.0f, 0.0f, 0.0f)};
+                    const V3 tn = tl_ok ? tr * neg(dtl) : v3(0.0f, 0.0f, 0.0f);
                     rv = L.col;                                    // Light::attenuate (light.cu:30-31)
                     // Unlit skip: when phong's factor (diffuse + specular) is zero in every
                     // channel -- the light behind the surface, no specular lobe -- the light's
@@ -935,7 +944,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     // marks it): no hit, so the light's term is phong's with the unshadowed
                     // light, the same signed zeros.
                     const DMat& mm = bv.mats[is_mat];
-                    fct = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl);
+                    fct = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl, tl, tn);
                     if (P.unlit_skip && fct.x == 0.0f && fct.y == 0.0f && fct.z == 0.0f && fct.w == 0.0f)
                         max_t = -INFINITY;
                     q = make_ray(at(to, THRESH), to.d);

@@ -60,11 +60,13 @@ RT_HD float dot4(V4 a, V4 b) {
     float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; s += a.w * b.w; return s;
 }
 
-RT_HD V3 reflect(V3 dir, V3 nrm) {                                   // linear.h:217-226
-    float d_len = len(dir);
-    V3 dn = normalized(dir), nn = normalized(nrm);
+// reflect's tail with |dir| and normalized(dir), normalized(nrm) given
+RT_HD V3 reflect_pre(float d_len, V3 dn, V3 nn) {
     V3 proj = dot(dn, nn) * nn;
     return d_len * normalized(dn - 2.0f * proj);
+}
+RT_HD V3 reflect(V3 dir, V3 nrm) {                                   // linear.h:217-226
+    return reflect_pre(len(dir), normalized(dir), normalized(nrm));
 }
 RT_HD V3 refract(V3 dir, V3 nrm, float from, float to, bool& tir) {  // linear.h:228-243
     float d_len = len(dir);
