@@ -2530,7 +2530,25 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
     const int waves_needed = P.n_groups;
-    int blocks = std::min(s->n_cu * per_cu, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
+    // Frames in flight: a launch issued while the scene's previous frame is still running takes
+    // half the CUs.  A persistent block holds its CU (the LDS image) until its slowest wave
+    // ends; fewer blocks, each running twice the groups, leave fewer CUs held by one wave's last
+    // group, and two frames' blocks still cover the GPU.  Measured with four in flight
+    // (tools/pipe_slices.py, per-rank ms per frame at N = 1/2/4/8, same box): 0.655-0.665 /
+    // 0.374 / 0.226 / 0.156-0.157 with every CU, 0.646-0.654 / 0.347-0.354 / 0.200-0.205 /
+    // 0.137-0.140 with half; 3/8, 5/8 and 3/4 of the CUs in between (profiles/r03/ab_grid/).
+    // A frame issued alone (no other frame running) keeps every CU.  Requiring two or three
+    // running frames instead of one measured the same (profiles/r03/ab_grid/grid2.log).
+    int cap = s->n_cu * per_cu;
+    if (s->n_slots >= 4) {
+        bool running = false;                                  // another frame of the scene in flight
+        for (int i = 1; i < s->n_slots && !running; i++) {
+            const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
+            running = s->slot_pending[sl] && hipEventQuery(s->slot_done[sl]) == hipErrorNotReady;
+        }
+        if (running) cap = std::max(1, cap / 2);
+    }
+    int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
     P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     // longest-first history (fast frames): valid while the launch layout is unchanged

@@ -129,14 +129,26 @@ class FramePipeline:
     copy; a host buffer is reused depth frames later, after its copy (and the caller's read)
     is done."""
 
-    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False):
+    def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False,
+                 streams=None):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
         self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(D)]
         # CPU tensors (the gloo tests of the multi-process logic): no streams, no events
         self.cuda = str(device).startswith("cuda")
-        self.streams = [torch.cuda.Stream(device=device) if self.cuda else None for _ in range(D)]
+        # streams: the render streams to reuse (at least `depth` of them; e.g. a later pipeline in
+        # the same process).  HIP spreads streams over GPU_MAX_HW_QUEUES hardware queues in the
+        # order they are created, and two render streams that share a queue serialise their
+        # frames (measured: 0.354 -> 0.42-0.44 ms per 2-way slice frame; DESIGN.md §4.1).  torch's
+        # stream pool hands out streams in creation order, and the first seven take distinct
+        # queues of eight (the null stream holds the first): create the pipeline early and reuse
+        # its streams rather than drawing new ones for each pipeline.
+        if streams is not None:
+            assert len(streams) >= D, (len(streams), D)
+            self.streams = list(streams)[:D]
+        else:
+            self.streams = [torch.cuda.Stream(device=device) if self.cuda else None for _ in range(D)]
         self.main = torch.cuda.current_stream(device) if self.cuda else None
         self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(D)]
                       if (world > 1 and rank == 0) else None)
