@@ -1928,6 +1928,10 @@ struct rt_scene {
     // flight keeps the poses its BVH was built from, and the next frame of a slot receives the
     // current poses by a stream-ordered copy (sync_slot_insts) from the slot's pinned staging.
     DInst* h_insts_pin = nullptr; float4* h_inst4_pin = nullptr;   // current slot's staging (pinned)
+#ifndef RT_OVERLAP_DEFAULT
+#define RT_OVERLAP_DEFAULT RT_OVERLAP_HALF   // (RT_OVERLAP_FULL: the A/B arm of round 3's policy)
+#endif
+    int overlap = RT_OVERLAP_DEFAULT;                                // rt_scene_set_overlap
     unsigned slot_inst_gen = 0;                  // instance generation the current slot's arrays hold
     unsigned inst_gen = 1;                       // generation of the host instance array (set_trans bumps it)
     unsigned shape_gen = 0;                      // generation n_real / fdepth were computed for
@@ -2538,9 +2542,13 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // 0.374 / 0.226 / 0.156-0.157 with every CU, 0.646-0.654 / 0.347-0.354 / 0.200-0.205 /
     // 0.137-0.140 with half; 3/8, 5/8 and 3/4 of the CUs in between (profiles/r03/ab_grid/).
     // A frame issued alone (no other frame running) keeps every CU.  Requiring two or three
-    // running frames instead of one measured the same (profiles/r03/ab_grid/grid2.log).
+    // running frames instead of one measured the same (profiles/r03/ab_grid/grid2.log).  A
+    // pipeline that copies every frame to the host measured 12% slower this way, with the copy
+    // anywhere (render stream, copy stream, high priority, fewer blit workgroups) and with the
+    // optional second half of the grid gated on later frames being queued
+    // (profiles/r03/ab_grid/readback.log): such callers set RT_OVERLAP_FULL.
     int cap = s->n_cu * per_cu;
-    if (s->n_slots >= 4) {
+    if (s->n_slots >= 4 && s->overlap == RT_OVERLAP_HALF) {
         bool running = false;                                  // another frame of the scene in flight
         for (int i = 1; i < s->n_slots && !running; i++) {
             const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
@@ -3238,6 +3246,13 @@ int rt_scene_set_frame_slots(rt_scene* s, int n) {
     for (auto& p : s->slot_pending) p = false;
     s->n_slots = n;
     return (n > 1 && s->uploaded) ? ensure_other_slot(s) : RT_OK;
+}
+
+int rt_scene_set_overlap(rt_scene* s, int policy) {
+    CHECK_SCENE(s);
+    if (policy != RT_OVERLAP_HALF && policy != RT_OVERLAP_FULL) return fail(RT_ERR_ARG, "overlap policy: RT_OVERLAP_HALF or RT_OVERLAP_FULL");
+    s->overlap = policy;
+    return RT_OK;
 }
 
 int rt_scene_set_devices(rt_scene* s, const int* devices, int n_devices, int n_ranks) {

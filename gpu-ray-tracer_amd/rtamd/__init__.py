@@ -35,7 +35,7 @@ SYMBOLS = [
     "rt_render_opts_default", "rt_render", "rt_update_scene", "rt_canvas_read", "rt_canvas_host_ptr",
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
-    "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_frame_work",
+    "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_scene_set_overlap", "rt_frame_work",
     "rt_scene_set_devices",
 ]
 
@@ -126,6 +126,7 @@ def lib():
     L.rt_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ip)]
     L.rt_device_count.argtypes = [ctypes.POINTER(ip)]
     L.rt_scene_set_frame_slots.argtypes = [vp, ip]
+    L.rt_scene_set_overlap.argtypes = [vp, ip]
     L.rt_frame_work.argtypes = [vp, ctypes.POINTER(RenderOpts), ctypes.POINTER(Work)]
     L.rt_scene_set_devices.argtypes = [vp, vp, ip, ip]
     _lib = L
@@ -393,6 +394,12 @@ class Scene:
         state (BVH, work counters, scheduling history), so frames issued on different streams
         overlap (rt_scene_set_frame_slots)."""
         _check(lib().rt_scene_set_frame_slots(self._h, int(n)))
+
+    def set_overlap(self, full):
+        """Grid of a frame issued while another frame of the scene runs (four slots): False =
+        half the CUs (default; device-resident pipelines), True = every CU (pipelines that
+        copy each frame to the host) (rt_scene_set_overlap)."""
+        _check(lib().rt_scene_set_overlap(self._h, 1 if full else 0))
 
     def timing_collect(self):
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()

@@ -123,14 +123,17 @@ class FramePipeline:
 
     readback=True keeps the reference's post-condition (update_scene returns with the frame
     host-readable, raytracer.cu:102-120 / canvas.cu:23-29) without giving up the overlap: the
-    finished frame (rank 0) is copied into pinned host buffer k % depth by an asynchronous
-    device-to-host copy -- on the render stream for one rank, on a copy stream after the
-    un-permute otherwise -- while later frames render.  `host_frame(k)` waits for frame k's
-    copy; a host buffer is reused depth frames later, after its copy (and the caller's read)
-    is done."""
+    finished frame (rank 0) is copied into pinned host buffer k % host_buffers by an
+    asynchronous device-to-host copy -- on the render stream for one rank, on a copy stream
+    after the un-permute otherwise -- while later frames render.  `host_frame(k)` waits for
+    frame k's copy; a host buffer is reused host_buffers frames later, after its copy (and the
+    caller's read) is done, so a consumer may read frames up to host_buffers - 1 behind the
+    last one issued.  host_buffers defaults to 2 x depth: the frames the consumer has not read
+    yet are the frames in flight, and a consumer only depth - 1 behind caps them at depth
+    including the copies (measured: DESIGN.md §4.1)."""
 
     def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False,
-                 streams=None):
+                 streams=None, host_buffers=None):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
@@ -157,10 +160,12 @@ class FramePipeline:
         self.outs = ([torch.empty((height, width), dtype=dtype, device=device) for _ in range(n_out)]
                      if (world > 1 and rank == 0) else None)
         self.out = self.outs[0] if self.outs else None
+        self.n_host = max(D, int(host_buffers)) if host_buffers else 2 * D
         if self.readback:
-            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=self.cuda) for _ in range(D)]
-            self.host_ev = [None] * D       # D2H copy of the frame last copied into each host buffer
-            self.host_no = [-1] * D         # its frame number
+            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=self.cuda) for _ in range(self.n_host)]
+            self.host_ev = [None] * self.n_host     # D2H copy of the frame last copied into each host buffer
+            self.host_no = [-1] * self.n_host       # its frame number
+            self.out_copy = [None] * D              # world > 1: the copy that last read each un-permute target
             self.copy_stream = torch.cuda.Stream(device=device) if (world > 1 and self.cuda) else None
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
@@ -185,14 +190,16 @@ class FramePipeline:
             return self.parts[self.last % self.depth] if self.last >= 0 else None
         return self.out
 
-    def _to_host(self, s, k, src, stream):
-        """Frame k (device buffer src, complete on `stream`) -> pinned host buffer s."""
-        if self.host_ev[s] is not None:
-            self.host_ev[s].synchronize()           # frame k - depth's copy is done (and was read)
+    def _to_host(self, k, src, stream):
+        """Frame k (device buffer src, complete on `stream`) -> pinned host buffer k % n_host."""
+        h = k % self.n_host
+        if self.host_ev[h] is not None:
+            self.host_ev[h].synchronize()           # frame k - n_host's copy is done (and was read)
         with self._on(stream):
-            self.host[s].copy_(src, non_blocking=self.cuda)
+            self.host[h].copy_(src, non_blocking=self.cuda)
             ev = self._event(stream)
-        self.host_ev[s], self.host_no[s] = ev, k
+        self.host_ev[h], self.host_no[h] = ev, k
+        return ev
 
     def _unpermute(self, s):
         if not self.pending[s]:
@@ -203,8 +210,8 @@ class FramePipeline:
             if self.rank == 0:
                 g = self.gbufs[s]
                 out = self.outs[s % len(self.outs)]
-                if self.readback and self.host_ev[s] is not None and self.cuda:
-                    self.main.wait_event(self.host_ev[s])   # frame k - depth's copy has read out
+                if self.readback and self.out_copy[s] is not None and self.cuda:
+                    self.main.wait_event(self.out_copy[s])  # frame k - depth's copy has read out
                 if self.H % self.world == 0:
                     out.view(self.rows, self.world, self.W).copy_(g.transpose(0, 1))
                 else:
@@ -216,7 +223,7 @@ class FramePipeline:
                 if self.readback:
                     if self.cuda:
                         self.copy_stream.wait_event(ev)
-                    self._to_host(s, self.pend_no[s], out, self.copy_stream)
+                    self.out_copy[s] = self._to_host(self.pend_no[s], out, self.copy_stream)
 
     def step(self, k, render):
         """Issue frame k: render(part, stream) enqueues the render of this rank's rows."""
@@ -227,7 +234,7 @@ class FramePipeline:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
             render(self.parts[s], st)
             if self.readback and self.world == 1:
-                self._to_host(s, k, self.parts[s], st)
+                self._to_host(k, self.parts[s], st)
             if self.world > 1:
                 if self.unperm[s] is not None and self.cuda:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]
@@ -241,13 +248,14 @@ class FramePipeline:
 
     def host_frame(self, k):
         """Frame k on the host (readback=True; rank 0): waits for its device-to-host copy.
-        Valid until frame k + depth is issued."""
+        Valid until frame k + host_buffers is issued."""
         s = k % self.depth
         if self.world > 1 and self.pending[s] and self.pend_no[s] == k:
             self._unpermute(s)
-        assert self.host_no[s] == k, (k, self.host_no[s])
-        self.host_ev[s].synchronize()
-        return self.host[s]
+        h = k % self.n_host
+        assert self.host_no[h] == k, (k, self.host_no[h])
+        self.host_ev[h].synchronize()
+        return self.host[h]
 
     def finish(self):
         """Complete every issued frame (stream-ordered on the main stream)."""

@@ -168,6 +168,15 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* opts, rt_work* work);
  * outputs.  Images are identical either way.  Waits for the device when changed. */
 int rt_scene_set_frame_slots(rt_scene* s, int n_slots);
 
+/* Grid of a frame issued while another frame of the scene is still running (four frame
+ * slots): RT_OVERLAP_HALF (default) = half the CUs, so that two frames' persistent blocks
+ * share the GPU and a block's tail (its slowest wave) holds fewer CUs; RT_OVERLAP_FULL =
+ * every CU, as a frame issued alone gets.  HALF measured faster for device-resident
+ * pipelines (frame -3%, row slices -4..-11%), FULL for pipelines that copy every frame to the
+ * host (-12%).  Images are identical either way.  Host-side state. */
+enum { RT_OVERLAP_HALF = 0, RT_OVERLAP_FULL = 1 };
+int rt_scene_set_overlap(rt_scene* s, int policy);
+
 /* Multi-GPU frames from one host process (the reference's single-device
  * update_scene, raytracer.cu:102-120, split over a node's GPUs).  After this call every
  * whole-frame rt_render / rt_update_scene of the scene renders n_ranks row-cyclic slices

@@ -72,7 +72,7 @@ def test_rows_partition_covers_frame_once():
             assert all(len(rtdist.rows_of(r, g, h)) <= rtdist.slice_height(g, h) for r in range(g))
 
 
-def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback):
+def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback, lag):
     import torch.distributed as dist
     from oracle_lib import Oracle
     import rtamd.dist as rtdist
@@ -93,13 +93,13 @@ def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback):
         n = 2 * depth + 2
         for k in range(n):
             pipe.step(k, render(k))
-            j = k - depth + 1                                # a host consumer depth - 1 frames behind
+            j = k - lag                                      # a host consumer `lag` frames behind
             if readback and rank == 0 and j >= 0:
                 got.append(pipe.host_frame(j).clone().numpy())
         last = pipe.finish()
         if rank == 0:
             if readback:
-                got += [pipe.host_frame(j).clone().numpy() for j in range(n - depth + 1, n)]
+                got += [pipe.host_frame(j).clone().numpy() for j in range(n - lag, n)]
             else:
                 got = [last.clone().numpy()]
             np.save(out_path, np.stack(got))
@@ -107,15 +107,17 @@ def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,h,depth,readback", [(2, 61, 3, False), (3, 60, 4, False), (2, 61, 3, True),
-                                                    (3, 61, 2, True)])
-def test_frame_pipeline_gather_across_processes(oracle, tmp_path, world, h, depth, readback):
+@pytest.mark.parametrize("world,h,depth,readback,lag", [(2, 61, 3, False, 0), (3, 60, 4, False, 0),
+                                                        (2, 61, 3, True, 2), (3, 61, 2, True, 1),
+                                                        (2, 61, 3, True, 5)])
+def test_frame_pipeline_gather_across_processes(oracle, tmp_path, world, h, depth, readback, lag):
     """rtamd.dist.FramePipeline (bench.py's default N > 1 path) across processes: frames in
     flight, asynchronous gathers into per-slot buffers, the un-permute one frame later, and
-    (readback) every frame's host copy -- the frame k that rank 0 reads is image + k."""
+    (readback) every frame's host copy -- the frame k that rank 0 reads is image + k, for a
+    consumer depth - 1 frames behind and one 2 x depth - 1 behind (the default host buffers)."""
     scene, w, spp = "world8_stress", 96, 2
     out_path = str(tmp_path / "frames.npy")
-    mp.spawn(_pipe_main, args=(world, _free_port(), scene, w, h, spp, out_path, depth, readback), nprocs=world,
+    mp.spawn(_pipe_main, args=(world, _free_port(), scene, w, h, spp, out_path, depth, readback, lag), nprocs=world,
              join=True)
     full = oracle.render(oracle.load(scene_path(scene), w, h), spp=spp, nthreads=4, want=("rgba",))["rgba"].view(np.int32)
     got = np.load(out_path)

@@ -153,11 +153,12 @@ def test_pipeline_moving_instances(gpu, oracle, depth):
         assert torch.equal(outs[k], refs[k]), k
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_pipeline_host_readback(gpu, world):
+@pytest.mark.parametrize("world,extra", [(1, 0), (2, 0), (1, 3), (2, 3)])
+def test_pipeline_host_readback(gpu, world, extra):
     """FramePipeline(readback=True): every frame reaches its pinned host buffer through the
     asynchronous copy (rank 0 of a world-2 split: after the gather and un-permute), equal to
-    the serial frame, while later frames are in flight."""
+    the serial frame, while later frames are in flight; `extra` more frames behind too (the
+    default host buffers are 2 x depth: bench.py's consumer is 2 x depth - 1 behind)."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
     import rtamd.dist as rtdist
@@ -179,11 +180,11 @@ def test_pipeline_host_readback(gpu, world):
         pipe.step(k, lambda buf, st: s.render_device(spp=spp, compact=True, rgba_ptr=buf.data_ptr(),
                                                      stream=st.cuda_stream, **kw))
         if k >= depth - 1:
-            j = k - depth + 2 if world > 1 else k - depth + 1
+            j = (k - depth + 2 if world > 1 else k - depth + 1) - extra
             if j >= 0:
                 assert torch.equal(pipe.host_frame(j), full), (k, j)
                 seen += 1
     pipe.finish()
     torch.cuda.synchronize()
     assert torch.equal(pipe.host_frame(7), full)
-    assert seen >= 4
+    assert seen >= 4 - extra
