@@ -98,6 +98,11 @@ def cpu_baseline(args, scene_path):
     t = time.perf_counter()
     fg = orc.render(s, semantics=0, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=nthr, want=())
     dg = time.perf_counter() - t
+    # the same CPU path row-split over the job's host cores (BASELINE.md §3's all-core variant;
+    # the reference's CPU path is one serial pixel loop, raytracer.cc:49-50)
+    t = time.perf_counter()
+    fc = orc.render(s, semantics=1, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=nthr, want=())
+    dc = time.perf_counter() - t
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
@@ -107,6 +112,8 @@ def cpu_baseline(args, scene_path):
         "sample": "%s %dx%d rows y%%%d==0 (%d rows), spp=1, CPU-path semantics of src/raytracer.cc "
                   "(oracle restatement), 1 thread; %.1f s, %d rays; extrapolated frame at %d spp: %.0f ms"
                   % (args.scene, args.width, args.height, k, rows, dt, rays, args.spp, dt * k * args.spp * 1e3),
+        "cpu_path_all_cores": {"value": int(fc["stats"][0]) / dc / 1e6, "unit": "Mrays/s", "cores": nthr,
+                               "seconds": round(dc, 2), "kind": "port"},
         "gpu_semantics_all_cores": {"value": int(fg["stats"][0]) / dg / 1e6, "unit": "Mrays/s", "cores": nthr,
                                     "seconds": round(dg, 2)},
         "cpu_model": cpu_model,
