@@ -36,8 +36,12 @@ import time
 # GPU_MAX_HW_QUEUES hardware queues (4 by default), and streams sharing a queue serialise.
 # Main + 4 render streams + the collective's stream need more than 4 (measured: three
 # frames in flight 1.49 ms/frame on 4 queues, 1.41 on 8).
-# (HIP's default, also the pool's box setting, is 4; RT_BENCH_HW_QUEUES overrides the 8 used here.)
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
+# HIP assigns streams to queues in creation order (zig-zag over the queues), so with 8 the
+# first seven streams after the null stream are distinct; 16 leaves room for the collective's
+# and the readback copy's streams on N > 1 ranks without a render stream sharing a queue
+# (8 vs 16 on one GPU: equal frame and slice times).
+# (HIP's default, also the pool's box setting, is 4; RT_BENCH_HW_QUEUES overrides the 16 used here.)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "16")
 import torch  # first: the HIP runtime torch loads is the one librt_amd.so binds to
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -332,8 +336,8 @@ def main():
                    "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bvh": use_bvh,
                    "parallelism": ("row-cyclic x%d + %s gather" % (world, "gloo host-staged" if gloo else "RCCL"))
                                   if world > 1 else "single GPU",
-                   # HIP hardware queues per process (HIP's and the pool's default is 4; bench.py sets 8
-                   # so that four render streams + main + collective each get a queue)
+                   # HIP hardware queues per process (HIP's and the pool's default is 4; bench.py sets 16
+                   # so that four render streams + main + collective + copy each get a queue)
                    "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1},
         "rays_unit": "reference-equivalent rays: every cast_ray of the reference's propagate_ray (SURVEY 8d), "
                      "counted by the counted kernel on the same frame",

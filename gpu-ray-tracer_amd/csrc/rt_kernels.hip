@@ -1881,6 +1881,41 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
 // Host side: scene object and the C ABI
 // ===========================================================================
 struct MultiDev;
+// Host framebuffer in pinned memory: rt_update_scene's device-to-host copy of the frame (the
+// reference's post-condition, raytracer.cu:102-120) is then one direct transfer; into pageable
+// memory HIP stages it in chunks through a bounce buffer.  Pageable fallback when pinning fails
+// (no HIP device: the scene is still built and exported, nothing is rendered).
+struct HostCanvas {
+    uint32_t* p = nullptr;
+    size_t n = 0;
+    bool pinned = false;
+    HostCanvas() = default;
+    HostCanvas(const HostCanvas&) = delete;
+    HostCanvas& operator=(const HostCanvas&) = delete;
+    ~HostCanvas() { release(); }
+    void release() {
+        if (p) { if (pinned) (void)hipHostFree(p); else free(p); }
+        p = nullptr; n = 0; pinned = false;
+    }
+    void assign(size_t m, uint32_t v) {
+        release();
+        if (!m) return;
+        if (hipHostMalloc((void**)&p, m * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();
+            p = static_cast<uint32_t*>(malloc(m * sizeof(uint32_t)));
+            if (!p) return;
+        }
+        n = m;
+        std::fill(p, p + m, v);
+    }
+    uint32_t* data() { return p; }
+    const uint32_t* data() const { return p; }
+    size_t size() const { return n; }
+    uint32_t operator[](size_t i) const { return p[i]; }
+};
+
 struct rt_scene {
     rt::Scene h;
     MultiDev* multi = nullptr;                   // rt_scene_set_devices: frames split over several GPUs
@@ -1919,7 +1954,7 @@ struct rt_scene {
     size_t d_out_px = 0;
     int n_leaf = 0;
     bool uploaded = false, bvh_valid = false;
-    std::vector<uint32_t> canvas;    // host framebuffer (Canvas buffer, canvas.cu:7)
+    HostCanvas canvas;               // host framebuffer (Canvas buffer, canvas.cu:7), pinned
     // Frame slots (rt_scene_set_frame_slots): with n > 1 slots, consecutive frames rotate
     // through n copies of the per-frame state (BVH, work counters, scheduling history), so a
     // frame on another stream can start on CUs freed by the previous frames' tails.  The

@@ -1,7 +1,7 @@
 """Per-rank frame throughput of an N-way row-cyclic slice with frames in flight, on one GPU
 (the render side of bench.py --gpus N; no gather).  NS / DEPTHS / RT_BENCH_HW_QUEUES env vars."""
 import os, sys, time, json
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "16")
 import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
