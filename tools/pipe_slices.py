@@ -11,7 +11,7 @@ p = os.path.join(ROOT, "scenes", "world8_stress.json")
 S = rtamd.Scene.load_json(p, 1920, 1080)
 # one set of render streams for every configuration: streams drawn later from torch's pool can
 # share a hardware queue, which serialises two frames in flight
-streams = [torch.cuda.Stream() for _ in range(4)]
+streams = [torch.cuda.Stream() for _ in range(max(int(x) for x in os.environ.get("DEPTHS", "1,2,4").split(",")))]
 for n in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
     rows = len(range(0, 1080, n))
     for depth in [int(x) for x in os.environ.get("DEPTHS", "1,2,4").split(",")]:
