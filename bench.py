@@ -7,7 +7,7 @@ Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit que
 
 One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
 rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
-the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined four deep
+the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined eight deep
 (rtamd.dist.FramePipeline, rt_scene_set_frame_slots): frame k+1 renders on another
 stream and starts on the CUs that the previous frames' longest pixel groups leave idle,
 and frame k's gather runs on the collective stream meanwhile.  The timed region ends after the last
@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
-    p.add_argument("--frames-in-flight", type=int, default=4, help="frame pipeline depth (1-4)")
+    p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -151,7 +151,7 @@ def main():
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
     frame_no = [0]
-    depth = max(1, min(4, args.frames_in_flight))
+    depth = max(1, min(8, args.frames_in_flight))
     overlap = not args.no_overlap and not gloo and depth > 1
     if overlap:                           # frames in flight (rtamd.dist.FramePipeline)
         scene.set_frame_slots(depth)

@@ -1971,7 +1971,7 @@ struct rt_scene {
     unsigned inst_gen = 1;                       // generation of the host instance array (set_trans bumps it)
     unsigned shape_gen = 0;                      // generation n_real / fdepth were computed for
 #ifndef RT_MAX_SLOTS
-#define RT_MAX_SLOTS 4
+#define RT_MAX_SLOTS 8
 #endif
     static constexpr int MAX_SLOTS = RT_MAX_SLOTS;
     struct Slot {

@@ -390,7 +390,7 @@ class Scene:
         _check(lib().rt_scene_set_devices(self._h, _ptr(d), int(d.size), int(n_ranks or d.size)))
 
     def set_frame_slots(self, n):
-        """1 (default) to 4: consecutive frames rotate through n copies of the per-frame
+        """1 (default) to 8: consecutive frames rotate through n copies of the per-frame
         state (BVH, work counters, scheduling history), so frames issued on different streams
         overlap (rt_scene_set_frame_slots)."""
         _check(lib().rt_scene_set_frame_slots(self._h, int(n)))

@@ -159,7 +159,7 @@ typedef struct rt_work {
  * variant (the fast kernel needs the ordered tree in LDS). */
 int rt_frame_work(rt_scene* s, const rt_render_opts* opts, rt_work* work);
 
-/* Frame slots (1 = default, up to 4).  The reference rebuilds its BVH inside every
+/* Frame slots (1 = default, up to 8).  The reference rebuilds its BVH inside every
  * update_scene call (raytracer.cu:103-119), so a frame owns per-frame state: BVH, work
  * counters and scheduling history.  With n slots, consecutive rt_render calls rotate
  * through n copies of that state.  Frames issued on other streams then overlap the

@@ -68,11 +68,11 @@ def test_cpp_shim_and_cli_compile_against_the_abi(tmp_path):
 
 
 def test_frame_slots_arguments(rt):
-    """rt_scene_set_frame_slots takes 1 to 4 (host-side state; no GPU needed)."""
+    """rt_scene_set_frame_slots takes 1 to 8 (host-side state; no GPU needed)."""
     s = rt.Scene.load_json(scene_path("world1"), 16, 16)
-    for n in (2, 4, 3, 1):
+    for n in (2, 4, 8, 3, 1):
         s.set_frame_slots(n)
-    for n in (0, 5):
+    for n in (0, 9):
         with pytest.raises(rt.RtError) as e:
             s.set_frame_slots(n)
         assert e.value.code == rt.RT_ERR_ARG

@@ -3,7 +3,7 @@ oracle (raytracer.cu:17-43 sample semantics: build-defined spp offsets, per-samp
 k-ordered sum, truncating RGBA8):
 
 - config 4 / the bench's headline: world8_stress 1920x1080 8 spp rendered exactly as bench.py
-  renders it -- four frame slots, frames on rotating streams (FramePipeline), fast kernels with
+  renders it -- eight frame slots, frames on rotating streams (FramePipeline), fast kernels with
   the sky pre-pass -- on one GPU, and as 2 / 8 row-cyclic rank slices reassembled;
 - config 3: world8 1920x1080 8 spp; config 2: world1 1920x1080 brute force (counters too);
 - config 5's sample mapping at a reduced size: world16 and world16_tex (textured mode) at
@@ -29,7 +29,7 @@ def stress_1080p(oracle):
     return oracle.render(oracle.load(scene_path("world8_stress"), W, H), spp=8, nthreads=NTHREADS)
 
 
-def _pipelined(gpu, scene, spp, world=1, rank=0, depth=4, n_frames=7, textures=False):
+def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=False):
     """This rank's rows of the last of n_frames frames issued as bench.py issues them."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
@@ -64,7 +64,7 @@ def test_bench_rank_slices_world8_stress_1080p(gpu, stress_1080p, world):
     through its own four-deep pipeline, reassembled as rank 0's un-permute does."""
     frame = np.zeros((H, W), np.uint32)
     for r in range(world):
-        frame[r::world] = _pipelined(gpu, "world8_stress", 8, world=world, rank=r, n_frames=5)
+        frame[r::world] = _pipelined(gpu, "world8_stress", 8, world=world, rank=r, n_frames=9)
     assert_frames_equal({"rgba": frame}, stress_1080p, keys=("rgba",), ctx=world)
 
 
@@ -72,7 +72,7 @@ def test_world8_1080p_8spp(gpu, oracle):
     s = gpu.Scene.load_json(scene_path("world8"), W, H)
     fr = s.render(spp=8, want=WANT, stats=False)
     assert_frames_equal(fr, oracle.render(oracle.load(scene_path("world8"), W, H), spp=8, nthreads=NTHREADS))
-    assert np.array_equal(_pipelined(gpu, "world8", 8, n_frames=5), fr["rgba"])
+    assert np.array_equal(_pipelined(gpu, "world8", 8, n_frames=9), fr["rgba"])
 
 
 def test_world1_1080p_brute_force(gpu, oracle):
