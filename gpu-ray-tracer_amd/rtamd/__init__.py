@@ -396,7 +396,7 @@ class Scene:
         _check(lib().rt_scene_set_frame_slots(self._h, int(n)))
 
     def set_overlap(self, full):
-        """Grid of a frame issued while another frame of the scene runs (four slots): False =
+        """Grid of a frame issued while another frame of the scene runs (four or more slots): False =
         half the CUs (default; device-resident pipelines), True = every CU (pipelines that
         copy each frame to the host) (rt_scene_set_overlap)."""
         _check(lib().rt_scene_set_overlap(self._h, 1 if full else 0))
