@@ -2037,6 +2037,7 @@ int padded(int n_t) {   // raytracer.cu:79: 1 << ceil(log2(n))
 
 int upload_inst4(rt_scene* s);
 int ensure_other_slot(rt_scene* s);
+int mirror_slot_caps(rt_scene* s);
 
 // TriAx records (rt_math.h) of the axis-plane triangle path: axis, plane coordinate,
 // shared-plane flag and the in-plane reject box with its host-checked error bound.
@@ -2251,6 +2252,8 @@ int sync_slot_insts(rt_scene* s, hipStream_t st) {
         if (!s->h_insts_pin) {
             HIPCHK(hipHostMalloc((void**)&s->h_insts_pin, n * sizeof(DInst), hipHostMallocDefault));
             HIPCHK(hipHostMalloc((void**)&s->h_inst4_pin, n * sizeof(float4), hipHostMallocDefault));
+            int r;
+            if (s->n_slots > 1 && (r = mirror_slot_caps(s)) != RT_OK) return r;
         } else if (s->slot_pending[s->cur_slot]) {
             HIPCHK(hipEventSynchronize(s->slot_done[s->cur_slot]));
         }
@@ -2304,6 +2307,53 @@ int ensure_other_slot(rt_scene* s) {
         HIPCHK(hipMalloc((void**)&o.d_inst4, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(float4)));
         o.slot_inst_gen = 0;                                 // filled by sync_slot_insts on first use
         o.work_zeroed = false; o.bvh_valid = false;
+    }
+    return mirror_slot_caps(s);                              // the current slot's grown buffers too
+}
+
+// The current slot grew a per-frame buffer (sky flags, live lists, history, pinned instance
+// staging) at its first frame of a new layout: give every other allocated slot the same
+// capacity now, so that their first frames -- possibly inside a steady pipeline -- allocate
+// nothing (an allocation there cost the first 8 frames of a run up to ~1 ms: hipFree waits for
+// the device, pinned allocations take milliseconds).  The slots' contents are reset on first
+// use as before (history key, instance generation).  Only growth reaches here: waiting for the
+// device before freeing a smaller buffer is a one-time cost per layout.
+int mirror_slot_caps(rt_scene* s) {
+    bool synced = false;
+    auto sync_once = [&]() -> hipError_t { if (synced) return hipSuccess; synced = true; return hipDeviceSynchronize(); };
+    for (int i = 0; i < s->n_slots; i++) {
+        if (i == s->cur_slot) continue;
+        rt_scene::Slot& o = s->store[i];
+        if (!o.d_work) continue;                              // not allocated (ensure_other_slot)
+        if (s->d_gsky && o.gsky_cap < s->gsky_cap) {
+            if (o.d_gsky) { HIPCHK(sync_once()); dfree(o.d_gsky); }
+            HIPCHK(hipMalloc((void**)&o.d_gsky, s->gsky_cap));
+            o.gsky_cap = s->gsky_cap;
+        }
+        if (s->d_live && o.live_cap < s->live_cap) {
+            if (o.d_live) { HIPCHK(sync_once()); dfree(o.d_live); }
+            HIPCHK(hipMalloc((void**)&o.d_live, (size_t)s->live_cap * sizeof(int)));
+            o.live_cap = s->live_cap;
+        }
+        if (s->d_hctl && o.hist_cap < s->hist_cap) {
+            if (o.d_hctl) {
+                HIPCHK(sync_once());
+                for (int q = 0; q < 2; q++) { dfree(o.d_hlist[q]); dfree(o.d_hflag[q]); }
+                dfree(o.d_hctl);
+            }
+            for (int q = 0; q < 2; q++) {
+                HIPCHK(hipMalloc((void**)&o.d_hlist[q], (size_t)s->hist_cap * sizeof(int)));
+                HIPCHK(hipMalloc((void**)&o.d_hflag[q], s->hist_cap));
+            }
+            HIPCHK(hipMalloc((void**)&o.d_hctl, 4 * sizeof(unsigned long long)));
+            o.hist_cap = s->hist_cap;
+            o.hist_key[0] = -1;                               // reset at the slot's first use
+        }
+        const size_t n = s->h.d_insts.size();
+        if (s->h_insts_pin && !o.h_insts_pin && n) {
+            HIPCHK(hipHostMalloc((void**)&o.h_insts_pin, n * sizeof(DInst), hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void**)&o.h_inst4_pin, n * sizeof(float4), hipHostMallocDefault));
+        }
     }
     return RT_OK;
 }
@@ -2605,7 +2655,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     if (!want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
         const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
         int r;
+        const int cap0 = s->hist_cap;
         if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
+        if (s->n_slots > 1 && s->hist_cap > cap0 && (r = mirror_slot_caps(s)) != RT_OK) return r;
         const int prev = s->hist_parity, next = 1 - prev;
         P.hist = 1;
         P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
@@ -2619,7 +2671,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
     const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
     if (sky) {
+        bool grew = false;
         if (P.n_groups > s->gsky_cap) {
+            grew = true;
             dfree(s->d_gsky);
             const int cap = (std::max(P.n_groups, 1024) + 3) & ~3;   // whole dwords (scalar loads)
             HIPCHK(hipMalloc((void**)&s->d_gsky, cap));
@@ -2628,12 +2682,14 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         const int sblocks = (P.n_groups + 63) / 64;
         const int lcap = (sblocks + NQ - 1) / NQ * 64;          // most groups of the blocks b = q mod NQ
         if ((long long)lcap * NQ > s->live_cap) {
+            grew = true;
             dfree(s->d_live);
             HIPCHK(hipMalloc((void**)&s->d_live, (size_t)lcap * NQ * sizeof(int)));
             s->live_cap = lcap * NQ;
         }
         P.gsky = s->d_gsky;
         P.live = s->d_live; P.live_cap = lcap;
+        if (s->n_slots > 1 && grew) { int r; if ((r = mirror_slot_caps(s)) != RT_OK) return r; }
         P.tpc = RT_TPC_LIVE;
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
         HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
