@@ -82,6 +82,24 @@ def parse():
     return p.parse_args()
 
 
+def cgroup_cpu_quota():
+    """CPUs this job's cgroup may use (cgroup v2 cpu.max = "quota period", v1 cfs files), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(args, scene_path):
     """The reference's CPU path (src/raytracer.cc semantics, restated in oracle/) on a
     bounded sample of the same workload, 1 thread -- the reference's CPU path is serial
@@ -98,7 +116,14 @@ def cpu_baseline(args, scene_path):
     dt = time.perf_counter() - t
     rays = int(fr["stats"][0])
     rows = len(range(0, args.height, k))
-    nthr = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    # every core this job may run on (its CPU affinity), not the machine's count: a GPU box shares
+    # its host between jobs and pins each to its share
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = cgroup_cpu_quota()              # a CPU-time quota caps the job below its affinity mask
+    nthr = max(1, min(affinity, quota) if quota else affinity)
     t = time.perf_counter()
     fg = orc.render(s, semantics=0, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=nthr, want=())
     dg = time.perf_counter() - t
@@ -120,7 +145,8 @@ def cpu_baseline(args, scene_path):
                                "seconds": round(dc, 2), "kind": "port"},
         "gpu_semantics_all_cores": {"value": int(fg["stats"][0]) / dg / 1e6, "unit": "Mrays/s", "cores": nthr,
                                     "seconds": round(dg, 2)},
-        "cpu_model": cpu_model,
+        "cpu_model": cpu_model, "nproc": os.cpu_count(), "affinity_cores": affinity, "cgroup_cpu_quota": quota,
+        "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
     }
 
 
@@ -351,6 +377,22 @@ def main():
         out["queries_traced_per_frame"] = int(queries)
         out["queries_traced_Mrays_s"] = round(queries * args.steps / elapsed / 1e6, 3)
         out["leaf_visits_traced_per_frame"] = int(leaf_lanes)
+        if rank == 0 and work.get("live_wave_queries"):
+            # lane occupancy of the wave-collective closest-hit query (rank 0's rows): every query,
+            # and the live groups' queries only (the sky groups' one all-lane query each is answered
+            # by the pre-pass in the product kernel); lanes by integrator phase; the live wave queries
+            # by active lanes (buckets of 8) with their child-pair steps and leaf visits
+            hw, hp, hl = work["hist_wave_queries"], work["hist_pair_steps"], work["hist_leaf_visits"]
+            out["query_occupancy"] = {
+                "all": round(work["queries"] / (64.0 * max(1, work["wave_queries"])), 4),
+                "live_groups": round(work["live_lanes"] / (64.0 * work["live_wave_queries"]), 4),
+                "lanes_by_phase": {"primary": work["lanes_primary"], "secondary": work["lanes_secondary"],
+                                   "shadow": work["lanes_shadow"], "unlit_skipped": work["lanes_unlit"]},
+                "live_wave_queries": work["live_wave_queries"],
+                "live_hist_active_lanes": ["%d-%d" % (8 * i + 1, 8 * i + 8) for i in range(8)],
+                "live_hist_wave_queries": hw, "live_hist_pair_steps": hp, "live_hist_leaf_visits": hl,
+                "pair_steps_below_half_occupancy": round(sum(hp[:4]) / max(1, sum(hp)), 4),
+                "source": "rt_frame_work (the fast kernel's profiling variant, untimed)"}
     if issue.get("SQ_INSTS_VALU"):
         # what bounds the kernel in fact: VALU issue plus dependent latency.
         # VALU wave-instructions per launch from the committed PMC profile, over this run's

@@ -69,6 +69,18 @@ constexpr int NQ = RT_NQ;                    // work queues (one per XCD dispatc
 // work counters: [16 q] queue q's tickets, [16 NQ] the heavy list's, [16 (NQ + 1 + q)] the
 // length of live-group list q (sky_kernel)
 constexpr int WORK_INTS = 16 * (2 * NQ + 1);
+// Statistics / profiling counters (d_stats): [0, 22) rt_stats and the PROF step counts and
+// cycle split (rt_experiment), [22, 24) spare, [24, 64) the PROF variant's query-occupancy
+// counters (PROF_* below, rt_frame_work).
+constexpr int STATS_N = 64;
+enum : int {
+    PROF_LANES_PRIMARY = 24, PROF_LANES_SECONDARY = 25, PROF_LANES_SHADOW = 26, PROF_LANES_UNLIT = 27,
+    PROF_LIVE_WQ = 28, PROF_LIVE_LANES = 29,
+    PROF_HIST_WQ = 30,      // [8] live wave queries by active lanes, buckets of 8 (1-8, 9-16, ..., 57-64)
+    PROF_HIST_PAIR = 38,    // [8] their child-pair steps
+    PROF_HIST_LEAF = 46,    // [8] their leaf visits
+    PROF_END = 54
+};
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -288,7 +300,7 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 // Per-lane work counters (rays/nodes/leaves/triangle tests, the reference's units) plus
 // wave-level step counts for the profiling experiment (query iterations, child-pair
 // steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
-struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary; };
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary, live; };
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
@@ -1027,7 +1039,30 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
         // (an unlit-skipped shadow step, max_t = -inf, takes no query)
         const bool qa = st == ST_WAIT_NORMAL || (st == ST_WAIT_SHADOW && max_t >= 0.0f);
+        const unsigned long long prof_p0 = wc.wpair, prof_l0 = wc.wleaf;
         const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(S, bv, qa, q, b, wc, occl, lim);
+        if (PROF && P.stats) {                                 // query occupancy (rt_frame_work)
+            const unsigned long long mp = __ballot(st == ST_WAIT_NORMAL && (fl & 1));
+            const unsigned long long mn = __ballot(st == ST_WAIT_NORMAL);
+            const unsigned long long ms = __ballot(st == ST_WAIT_SHADOW && qa);
+            const unsigned long long mu = __ballot(st == ST_WAIT_SHADOW && !qa);
+            const int na = __popcll(mn | ms);
+            if (lane_id_fresh() == 0) {
+                KTP& Pp = kparams();
+                atomicAdd(&Pp.stats[PROF_LANES_PRIMARY], (unsigned long long)__popcll(mp));
+                atomicAdd(&Pp.stats[PROF_LANES_SECONDARY], (unsigned long long)__popcll(mn & ~mp));
+                atomicAdd(&Pp.stats[PROF_LANES_SHADOW], (unsigned long long)__popcll(ms));
+                atomicAdd(&Pp.stats[PROF_LANES_UNLIT], (unsigned long long)__popcll(mu));
+                if (wc.live && na > 0) {
+                    const int bk = (na - 1) >> 3;
+                    atomicAdd(&Pp.stats[PROF_LIVE_WQ], 1ull);
+                    atomicAdd(&Pp.stats[PROF_LIVE_LANES], (unsigned long long)na);
+                    atomicAdd(&Pp.stats[PROF_HIST_WQ + bk], 1ull);
+                    atomicAdd(&Pp.stats[PROF_HIST_PAIR + bk], wc.wpair - prof_p0);
+                    atomicAdd(&Pp.stats[PROF_HIST_LEAF + bk], wc.wleaf - prof_l0);
+                }
+            }
+        }
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -1346,6 +1381,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                 }
                 break;                                         // sum_c = sum_r = 0
             }
+            // PROF: the group is live when some primary enters the tree's root (the sky pre-pass's
+            // test); occupancy counters are taken over live groups' queries only
+            if (PROF && FT) wc.live = __ballot(ft_root_hit(S, bv, act, r0)) != 0;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
             V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);
@@ -2215,7 +2253,7 @@ int upload(rt_scene* s) {
     if ((r = up(s->d_tri_ax, tri_axis_records(h))) != RT_OK) return r;
     if ((r = up(s->d_mesh_box, mesh_boxes(h))) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
-    HIPCHK(hipMalloc((void**)&s->d_stats, 24 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&s->d_stats, STATS_N * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
     for (auto& e : s->slot_done) if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -3275,7 +3313,7 @@ int rt_render(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
         select_slot(s, (s->cur_slot + 1) % s->n_slots);
     }
     if ((r = begin_frame(s, st, false)) != RT_OK) return r;  // after the slot's previous frame, current poses
-    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
+    if (timed) { HIPCHK(hipMemsetAsync(s->d_stats, 0, STATS_N * sizeof(unsigned long long), st)); HIPCHK(hipEventRecord(s->ev[0], st)); }
     if (o->use_bvh && (o->rebuild_bvh || !s->bvh_valid)) {
         if ((r = build_bvh(s, st, te ? te[0] : nullptr, te ? te[1] : nullptr)) != RT_OK) {
             if (te) s->tev_used -= 4;                            // the frame's events stay unrecorded
@@ -3470,7 +3508,7 @@ int rt_experiment(rt_scene* s, int which, int spp, int reps, double* ms, uint64_
         if ((r = build_bvh(s, sstream(s))) != RT_OK) return r;
         float total = 0;
         for (int i = 0; i < reps; i++) {
-            HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), sstream(s)));
+            HIPCHK(hipMemsetAsync(s->d_stats, 0, STATS_N * sizeof(unsigned long long), sstream(s)));
             HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), sstream(s)));
             HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), sstream(s)));
             HIPCHK(hipEventRecord(s->ev[0], sstream(s)));
@@ -3508,7 +3546,7 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* o, rt_work* w) {
     r = begin_frame(s, st, true);                             // nothing else in flight on this slot
     if (r == RT_OK) r = build_bvh(s, st);
     if (r == RT_OK) {
-        HIPCHK(hipMemsetAsync(s->d_stats, 0, 24 * sizeof(unsigned long long), st));
+        HIPCHK(hipMemsetAsync(s->d_stats, 0, STATS_N * sizeof(unsigned long long), st));
         HIPCHK(hipMemsetAsync(s->d_stats + 15, 0xff, sizeof(unsigned long long), st));
         HIPCHK(hipMemsetAsync(s->d_stats + 19, 0xff, sizeof(unsigned long long), st));
         rt_render_opts oo = *o;
@@ -3516,7 +3554,7 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* o, rt_work* w) {
         r = launch_trace(s, oo, st, d_rgba, nullptr, -1, -1, false, -1, nullptr, nullptr, true);
     }
     if (r == RT_OK) r = end_frame(s, st);
-    unsigned long long v[22] = {};
+    unsigned long long v[STATS_N] = {};
     if (r == RT_OK) {
         HIPCHK(hipStreamSynchronize(st));
         HIPCHK(hipMemcpy(v, s->d_stats, sizeof v, hipMemcpyDeviceToHost));
@@ -3527,6 +3565,14 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* o, rt_work* w) {
     w->queries = v[0]; w->wave_queries = v[4]; w->pair_steps = v[5]; w->leaf_visits = v[6]; w->tri_iters = v[7];
     w->leaf_lanes = v[2];
     w->scene_bytes = lds_bytes(view_of(s, true), true, true);   // the scene image a block stages
+    w->lanes_primary = v[PROF_LANES_PRIMARY]; w->lanes_secondary = v[PROF_LANES_SECONDARY];
+    w->lanes_shadow = v[PROF_LANES_SHADOW]; w->lanes_unlit = v[PROF_LANES_UNLIT];
+    w->live_wave_queries = v[PROF_LIVE_WQ]; w->live_lanes = v[PROF_LIVE_LANES];
+    for (int i = 0; i < 8; i++) {
+        w->hist_wave_queries[i] = v[PROF_HIST_WQ + i];
+        w->hist_pair_steps[i] = v[PROF_HIST_PAIR + i];
+        w->hist_leaf_visits[i] = v[PROF_HIST_LEAF + i];
+    }
     return RT_OK;
 }
 

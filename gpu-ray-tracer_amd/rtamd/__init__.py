@@ -66,10 +66,20 @@ class Stats(ctypes.Structure):
 class Work(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_uint64), ("wave_queries", ctypes.c_uint64), ("pair_steps", ctypes.c_uint64),
                 ("leaf_visits", ctypes.c_uint64), ("leaf_lanes", ctypes.c_uint64), ("tri_iters", ctypes.c_uint64),
-                ("scene_bytes", ctypes.c_uint64)]
+                ("scene_bytes", ctypes.c_uint64),
+                # query occupancy (ABI 3)
+                ("lanes_primary", ctypes.c_uint64), ("lanes_secondary", ctypes.c_uint64),
+                ("lanes_shadow", ctypes.c_uint64), ("lanes_unlit", ctypes.c_uint64),
+                ("live_wave_queries", ctypes.c_uint64), ("live_lanes", ctypes.c_uint64),
+                ("hist_wave_queries", ctypes.c_uint64 * 8), ("hist_pair_steps", ctypes.c_uint64 * 8),
+                ("hist_leaf_visits", ctypes.c_uint64 * 8)]
 
     def as_dict(self):
-        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = [int(x) for x in v] if k.startswith("hist_") else int(v)
+        return d
 
 
 _lib = None

@@ -22,7 +22,9 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+/* 3: rt_work gained the query-occupancy fields; RT_EXPORT_TRIS / RT_EXPORT_TEXCOORDS list
+ *    triangles in the flattened mesh order (the index space of hit_tri) */
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -154,6 +156,18 @@ typedef struct rt_work {
     uint64_t tri_iters;     /* wave-level triangle-loop iterations */
     uint64_t scene_bytes;   /* the scene the fast kernel reads: ordered-tree records, instance records,
                                triangles, meshes, materials, lights (staged into each block's LDS) */
+    /* Query occupancy (ABI 3).  Lanes by integrator phase over every wave query: */
+    uint64_t lanes_primary;    /* primary-ray queries (sample's first NORMAL frame) */
+    uint64_t lanes_secondary;  /* reflection / refraction NORMAL-frame queries */
+    uint64_t lanes_shadow;     /* traced shadow segments */
+    uint64_t lanes_unlit;      /* shadow steps the unlit skip answers without a query */
+    /* Over the wave queries of live groups only (some primary enters the tree's root; the sky
+     * groups the pre-pass answers are left out): */
+    uint64_t live_wave_queries;
+    uint64_t live_lanes;       /* queries issued in them: occupancy = live_lanes / (64 live_wave_queries) */
+    uint64_t hist_wave_queries[8];  /* live wave queries by active lanes: 1-8, 9-16, ..., 57-64 */
+    uint64_t hist_pair_steps[8];    /* their child-pair steps */
+    uint64_t hist_leaf_visits[8];   /* their leaf visits */
 } rt_work;
 /* BVH frames with 1 <= spp <= 64, untextured; RT_ERR_STATE when the scene has no profiling
  * variant (the fast kernel needs the ordered tree in LDS). */

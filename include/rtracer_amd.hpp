@@ -7,14 +7,19 @@
 //   renv::gpu::Scene::free, scene->get_environment().get_canvas() / get_camera()
 //                                                    (include/rayenv/gpu/scene.h:55-69, environment.h:75-83,
 //                                                     canvas.h:17-44, entity.h:49-74)
-// compiles against this header unchanged in the calls it makes (main.cc:45-77, 140-184).
+// compiles against this header unchanged in the calls its GPU path makes (main.cc:61-77, 81-216,
+// including the camera moves and Canvas::get_surface when SDL.h comes first).  The CPU
+// renderer (rtracer::cpu, procedural::cpu, renv::cpu::Scene; main.cc:45-60) is not shipped
+// and not declared here: a caller drops its `-s` branch.
 // The reference asserts on errors; so does this shim (message from rt_last_error()).
 // Header-only; link with librt_amd.so.  Types are the reference's names with just the
 // members these calls use.
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <initializer_list>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -31,27 +36,53 @@ inline void check(int rc, const char* what) {
 }  // namespace rtamd_detail
 
 namespace rmath {
-template <class T> struct Vec3 {
-    T v[3] = {T(0), T(0), T(0)};
-    Vec3() = default;
-    Vec3(std::initializer_list<T> l) { int i = 0; for (T x : l) if (i < 3) v[i++] = x; }
-    T operator[](int i) const { return v[i]; }
-    T& operator[](int i) { return v[i]; }
+// The vector / quaternion / ray operations the reference's callers use on the host
+// (main.cc:140-180 moves and turns the camera with them), with linear.h / geometry.h's
+// semantics: Vec(initializer_list) fills leading coordinates, normalized() returns the zero
+// vector below the 1e-5 threshold (linear.h:159-167), Quat(axis, theta) = (axis sin(theta/2),
+// cos(theta/2)) (geometry.h:36-41), Quat * Quat is the Hamilton product (geometry.h:150-170),
+// Ray's direction is normalized at construction (geometry.h:216).
+constexpr double THRESHOLD = 1E-5f;
+template <class T, int Dim> class Vec {
+    T c_[Dim];
+public:
+    Vec() { for (int i = 0; i < Dim; i++) c_[i] = T(0); }
+    Vec(std::initializer_list<T> l) : Vec() { int i = 0; for (T x : l) { if (i >= Dim) break; c_[i++] = x; } }
+    static Vec zero() { return Vec(); }
+    T operator[](int i) const { return c_[i]; }
+    T& operator[](int i) { return c_[i]; }
+    friend Vec operator+(const Vec& a, const Vec& b) { Vec r; for (int i = 0; i < Dim; i++) r.c_[i] = a.c_[i] + b.c_[i]; return r; }
+    friend Vec operator-(const Vec& a, const Vec& b) { Vec r; for (int i = 0; i < Dim; i++) r.c_[i] = a.c_[i] - b.c_[i]; return r; }
+    friend Vec operator*(T k, const Vec& v) { Vec r; for (int i = 0; i < Dim; i++) r.c_[i] = k * v.c_[i]; return r; }
+    friend Vec operator-(const Vec& v) { return T(-1) * v; }
+    T squared_norm() const { T s = 0; for (int i = 0; i < Dim; i++) s += c_[i] * c_[i]; return s; }
+    T len() const { return std::sqrt(squared_norm()); }
+    Vec normalized() const { const T l = len(); return l > THRESHOLD ? (1 / l) * *this : Vec(); }
 };
-template <class T> struct Vec4 {
-    T v[4] = {T(0), T(0), T(0), T(0)};
-    Vec4() = default;
-    Vec4(std::initializer_list<T> l) { int i = 0; for (T x : l) if (i < 4) v[i++] = x; }
-    T operator[](int i) const { return v[i]; }
-    T& operator[](int i) { return v[i]; }
-};
-template <class T> struct Quat {          // (i, j, k, r) as geometry.h:143-181
+template <class T> using Vec3 = Vec<T, 3>;
+template <class T> using Vec4 = Vec<T, 4>;
+template <class T> struct Quat {          // (i, j, k, r) as geometry.h:20-181
     T i = 0, j = 0, k = 0, r = 1;
     Quat() = default;
     Quat(T i_, T j_, T k_, T r_) : i(i_), j(j_), k(k_), r(r_) {}
+    Quat(Vec3<T> axis, T theta) {
+        const T hc = std::cos(0.5f * theta), hs = std::sin(0.5f * theta);
+        i = axis[0] * hs; j = axis[1] * hs; k = axis[2] * hs; r = hc;
+    }
     static Quat identity() { return Quat(); }
+    friend Quat operator*(const Quat& a, const Quat& b) {
+        return Quat(a.i * b.r + a.r * b.i + a.j * b.k - a.k * b.j, a.j * b.r + a.r * b.j + a.k * b.i - a.i * b.k,
+                    a.k * b.r + a.r * b.k + a.i * b.j - a.j * b.i, a.r * b.r - a.i * b.i - a.j * b.j - a.k * b.k);
+    }
 };
-template <class T> struct Ray { Vec3<T> origin, direction; };
+template <class T> class Ray {
+    Vec3<T> o_, d_;
+public:
+    Ray() = default;
+    Ray(Vec3<T> origin, Vec3<T> direction) : o_(origin), d_(direction.normalized()) {}
+    Vec3<T> origin() const { return o_; }
+    Vec3<T> direction() const { return d_; }
+};
 }  // namespace rmath
 
 namespace rprimitives {
@@ -98,6 +129,16 @@ public:
     // The packed RGBA8 framebuffer (R<<24|G<<16|B<<8|A, row-major), the buffer the
     // reference hands to SDL in get_surface (canvas.cu:23-29).
     const std::uint32_t* get_buffer() const { return rt_canvas_host_ptr(s_); }
+#if defined(SDL_h_)
+    // Canvas::get_surface (canvas.cu:23-29), declared when SDL.h is included first (main.cc:1
+    // does): an SDL surface over the host framebuffer, 32 bits per pixel, R in bits 31..24
+    // (Color::rmask..amask, color.cu:38-56).  The buffer stays put across frames: each
+    // update_scene refreshes what the surface shows, as the reference's managed canvas does.
+    void get_surface(SDL_Surface** surface) {
+        *surface = SDL_CreateRGBSurfaceFrom(const_cast<std::uint32_t*>(get_buffer()), w_, h_, 32, 4 * w_,
+                                            0xff000000u, 0x00ff0000u, 0x0000ff00u, 0x000000ffu);
+    }
+#endif
 };
 
 class Camera {                            // camera.h (an Entity)
@@ -143,13 +184,10 @@ public:
     rmath::Ray<float> up() const { return axis(1); }
     rmath::Ray<float> forward() const { return axis(2); }
 private:
-    rmath::Ray<float> axis(int which) const {
+    rmath::Ray<float> axis(int which) const {    // camera.cu:11-31: Ray(pos, axis)
         float a[3][3];
         rtamd_detail::check(rt_camera_axes(s_, a[0], a[1], a[2]), "Camera axes");
-        rmath::Ray<float> r;
-        r.origin = pos();
-        r.direction = {a[which][0], a[which][1], a[which][2]};
-        return r;
+        return rmath::Ray<float>(pos(), {a[which][0], a[which][1], a[which][2]});
     }
 };
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == 2
+    assert rt.lib().rt_abi_version() == 3
 
 
 def test_library_is_gfx950_code(rt):
@@ -61,7 +61,8 @@ def test_cpp_shim_and_cli_compile_against_the_abi(tmp_path):
     import subprocess
     inc = os.path.join(ROOT, "include")
     libdir = os.path.join(ROOT, "gpu-ray-tracer_amd")
-    for src in (os.path.join(ROOT, "tests", "shim_world.cpp"), os.path.join(libdir, "cli", "rtracer.cpp")):
+    for src in (os.path.join(ROOT, "tests", "shim_world.cpp"), os.path.join(ROOT, "tests", "shim_main.cpp"),
+                os.path.join(libdir, "cli", "rtracer.cpp")):
         r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, src, "-o", str(tmp_path / "a.out"),
                             "-L", libdir, "-lrt_amd"], capture_output=True, text=True)
         assert r.returncode == 0, r.stderr

@@ -126,3 +126,29 @@ def test_cli_multi_device_slices(oracle, tmp_path, ranks):
     rgba = o["rgba"]
     exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
     assert np.array_equal(_ppm_rgb(out), exp)
+
+
+def test_cpp_shim_main_cc_calls(oracle, tmp_path):
+    """The reference front end's GPU-path calls through the shim (tests/shim_main.cpp: generate,
+    update_scene, Canvas::get_surface over an SDL test double, main.cc's key and mouse camera
+    moves, debug_cast): the frame the surface shows after the moves is the oracle's frame at the
+    camera pose the program reports."""
+    exe = str(tmp_path / "shim_main")
+    inc = os.path.join(ROOT, "include")
+    libdir = os.path.join(ROOT, "gpu-ray-tracer_amd")
+    r = _run(["g++", "-O1", "-std=c++17", "-I", inc, os.path.join(ROOT, "tests", "shim_main.cpp"), "-o", exe,
+              "-L", libdir, "-lrt_amd", "-Wl,-rpath," + libdir])
+    assert r.returncode == 0, r.stderr
+    out = str(tmp_path / "m.bin")
+    W, H = 160, 100
+    r = _run([exe, scene_path("world8_stress"), str(W), str(H), out])
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Loaded scene" in r.stdout and "shooting a ray" in r.stdout
+    raw = np.fromfile(out, np.uint8)
+    frame = raw[:4 * W * H].view(np.uint32).reshape(H, W)
+    pose = raw[4 * W * H:].view(np.float32)
+    o = oracle.load(scene_path("world8_stress"), W, H)
+    o.set_camera(pose[:3], pose[3:7])
+    exp = oracle.render(o, spp=1, nthreads=8, want=("rgba",))["rgba"]
+    assert np.array_equal(frame, exp)
+    assert (frame != 0).any()

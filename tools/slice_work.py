@@ -10,10 +10,11 @@ S = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", "world8_stress.json"), 19
 full = S.frame_work(spp=8)
 print(json.dumps({"n": 1, **full}))
 for n in (2, 4, 8):
-    tot = {k: 0 for k in full}
+    tot = {k: ([0] * len(v) if isinstance(v, list) else 0) for k, v in full.items()}
     for r in range(n):
         w = S.frame_work(spp=8, row0=r, row_step=n)
         for k in w:
-            tot[k] += w[k]
+            tot[k] = [a + b for a, b in zip(tot[k], w[k])] if isinstance(w[k], list) else tot[k] + w[k]
     print(json.dumps({"n": n, **{k: v for k, v in tot.items()},
-                      "ratio_to_full": {k: round(tot[k] / max(1, full[k]), 3) for k in full if k != "scene_bytes"}}))
+                      "ratio_to_full": {k: round(tot[k] / max(1, full[k]), 3) for k in full
+                                       if k != "scene_bytes" and not isinstance(full[k], list)}}))
