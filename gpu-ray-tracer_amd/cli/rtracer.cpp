@@ -2,7 +2,7 @@
 //
 //   rtracer -c world8.json [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K]
 //           [--width W --height H] [--out frame.ppm] [--debug X,Y] [--textures [ATLAS.png]]
-//           [--gpus N [--ranks R]]
+//           [--gpus N [--ranks R]] [--in-flight D]
 //
 // -c config (worldN.json), -b benchmark (one timed frame, "Time: X ms" as main.cc:210-216),
 // -r unoptimize (brute force, no BVH), -d kernel dimension (accepted; the HIP path
@@ -14,6 +14,11 @@
 // --textures turns on the build-defined textured shading mode with the scene's atlas
 // (or the given PNG).  --gpus N splits every frame row-cyclically over devices 0..N-1 of this
 // process (R slices, default N; RCCL gather to device 0: rtracer::gpu::use_devices).
+// --in-flight D (timing, build extension): --frames frames issued asynchronously with D in
+// flight (rt_scene_set_frame_slots), each into its own device buffer on its own stream, then
+// one wait; prints the time per frame and per slice.  --out then writes the last frame.
+#include <hip/hip_runtime_api.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -26,7 +31,8 @@
 static void usage() {
     std::fprintf(stderr,
                  "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
-                 "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]] [--gpus N [--ranks R]]\n");
+                 "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]] [--gpus N [--ranks R]]\n"
+                 "               [--in-flight D]\n");
 }
 
 static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
@@ -49,7 +55,7 @@ int main(int argc, char** argv) {
     std::string config, out;
     bool bench = false, unopt = false, serial = false, textures = false;
     std::string atlas;
-    int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1, gpus = 1, ranks = 0;
+    int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1, gpus = 1, ranks = 0, in_flight = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&](const char* name) -> const char* {
@@ -68,6 +74,7 @@ int main(int argc, char** argv) {
         else if (a == "--out") out = val("--out");
         else if (a == "--gpus") gpus = std::atoi(val("--gpus"));
         else if (a == "--ranks") ranks = std::atoi(val("--ranks"));
+        else if (a == "--in-flight") in_flight = std::atoi(val("--in-flight"));
         else if (a == "--textures") {
             textures = true;
             if (i + 1 < argc && argv[i + 1][0] != '-') atlas = argv[++i];
@@ -82,7 +89,10 @@ int main(int argc, char** argv) {
                              "restated in oracle/ for testing only\n");
         return 2;
     }
-    if (frames < 1 || spp < 1 || gpus < 1 || ranks < 0) { usage(); return 2; }
+    if (frames < 1 || spp < 1 || gpus < 1 || ranks < 0 || in_flight < 0 || in_flight > 8) { usage(); return 2; }
+    // frames in flight use a stream each: HIP maps streams round-robin onto GPU_MAX_HW_QUEUES
+    // hardware queues (4 by default), and streams sharing a queue serialise
+    if (in_flight > 1) setenv("GPU_MAX_HW_QUEUES", "16", 0);
 
     // procedural::gpu::generate with optional canvas override; a bad config is reported
     // and exits (the reference asserts)
@@ -107,6 +117,45 @@ int main(int argc, char** argv) {
     }
 
     std::vector<uint32_t> host;
+    if (in_flight > 0) {                                   // timing: D frames in flight
+        const int D = in_flight;
+        rtamd_detail::check(rt_scene_set_frame_slots(handle, D), "rt_scene_set_frame_slots");
+        std::vector<hipStream_t> st(D);
+        std::vector<uint32_t*> buf(D);
+        for (int k = 0; k < D; k++) {
+            if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
+                hipMalloc((void**)&buf[k], (size_t)W * H * 4) != hipSuccess) { std::fprintf(stderr, "HIP allocation failed\n"); return 1; }
+        }
+        long long f = 0;
+        auto issue = [&]() {
+            rt_render_opts o;
+            rt_render_opts_default(&o);
+            o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
+            o.rgba = buf[f % D]; o.stream = st[f % D];
+            rtamd_detail::check(rt_render(handle, &o, nullptr), "rt_render");
+            f++;
+        };
+        auto wait_all = [&]() { for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]); };
+        for (int k = 0; k < 2 * D; k++) issue();          // warm-up: slots, streams, scheduling history
+        wait_all();
+        auto from = std::chrono::high_resolution_clock::now();
+        for (int k = 0; k < frames; k++) issue();
+        wait_all();
+        auto to = std::chrono::high_resolution_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(to - from).count() / frames;
+        const int slices = (gpus > 1 || ranks > 1) ? (ranks > 0 ? ranks : gpus) : 1;
+        std::printf("In flight %d: %.4f ms/frame, %.4f ms per slice (%d slices on %d GPU(s), %d frames)\n", D, ms,
+                    ms * gpus / slices, slices, gpus, frames);
+        if (!out.empty()) {
+            host.resize((size_t)W * H);
+            if (hipMemcpy(host.data(), buf[(f - 1) % D], host.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+                !write_ppm(out.c_str(), host.data(), W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
+        }
+        for (int k = 0; k < D; k++) { (void)hipStreamDestroy(st[k]); (void)hipFree(buf[k]); }
+        renv::gpu::Scene::free(*scene);
+        delete scene;
+        return 0;
+    }
     auto draw = [&]() {
         if (spp == 1 && !textures) {
             rtracer::gpu::update_scene(scene, dim, !unopt);

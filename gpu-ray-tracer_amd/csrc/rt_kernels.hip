@@ -2253,6 +2253,7 @@ int upload(rt_scene* s) {
     if ((r = up(s->d_tri_ax, tri_axis_records(h))) != RT_OK) return r;
     if ((r = up(s->d_mesh_box, mesh_boxes(h))) != RT_OK) return r;
     HIPCHK(hipMalloc((void**)&s->d_tree, 2 * nl * sizeof(Box)));
+    if (s->n_leaf > BVH_WG_LEAVES) HIPCHK(hipMalloc(&s->d_bscratch, bvh_large_scratch_bytes(s->n_leaf)));
     HIPCHK(hipMalloc((void**)&s->d_stats, STATS_N * sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void**)&s->d_canvas, (size_t)h.cam.W * h.cam.H * sizeof(uint32_t)));
     HIPCHK(hipMalloc((void**)&s->d_dbg, 4096 * sizeof(int)));
@@ -2343,6 +2344,8 @@ int ensure_other_slot(rt_scene* s) {
         HIPCHK(hipMalloc((void**)&o.d_work, WORK_INTS * sizeof(int)));
         HIPCHK(hipMalloc((void**)&o.d_insts, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(DInst)));
         HIPCHK(hipMalloc((void**)&o.d_inst4, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(float4)));
+        // the grid-wide build's sort buffers now, not at the slot's first frame inside a pipeline
+        if (s->n_leaf > BVH_WG_LEAVES && !o.d_bscratch) HIPCHK(hipMalloc(&o.d_bscratch, bvh_large_scratch_bytes(s->n_leaf)));
         o.slot_inst_gen = 0;                                 // filled by sync_slot_insts on first use
         o.work_zeroed = false; o.bvh_valid = false;
     }
@@ -2855,25 +2858,49 @@ struct MultiDev {
     std::vector<int> devices;
     int n_ranks = 1, per_dev = 1, rows_max = 0, W = 0, H = 0;
     std::vector<rt_scene*> reps;                 // reps[0] = the scene itself; reps[i > 0] owned replicas
-    std::vector<hipStream_t> streams;
-    std::vector<uint32_t*> sbuf;                 // per device: per_dev slices of rows_max x W
-    uint32_t* gbuf = nullptr;                    // device 0: n_ranks slices
-    std::vector<ncclComm_t> comms;
     std::vector<unsigned> inst_gen;              // host instance generation each replica holds
+    std::vector<ncclComm_t> comms;               // one per device (ncclCommInitAll: rank = device order)
+    // Frames in flight: the scene's frame slots (rt_scene_set_frame_slots) give `depth`; frame f
+    // uses slot k = f % depth -- its own stream per device, slice buffers and gather buffer -- so
+    // frame f + 1 renders while frame f gathers and un-permutes.  A slot's stream orders frame f
+    // after frame f - depth, the last user of the slot's buffers.
+    int depth = 0;
+    long long frame = 0;
+    std::vector<std::vector<hipStream_t>> streams;   // [device][slot]
+    std::vector<std::vector<uint32_t*>> sbuf;        // [device][slot]: per_dev slices of rows_max x W
+    std::vector<uint32_t*> gbuf;                     // [slot], device 0: n_ranks slices
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;    // device 0: caller's stream -> frame -> caller's stream
 };
+
+namespace {
+// The per-slot streams and buffers (and their device work) released; the replicas and the
+// communicators stay.
+void free_multi_slots(MultiDev* m) {
+    for (size_t i = 0; i < m->streams.size(); i++) {
+        (void)hipSetDevice(m->devices[i]);
+        for (hipStream_t st : m->streams[i]) if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); }
+        if (i < m->sbuf.size()) for (uint32_t* b : m->sbuf[i]) if (b) (void)hipFree(b);
+    }
+    (void)hipSetDevice(m->devices[0]);
+    for (uint32_t* b : m->gbuf) if (b) (void)hipFree(b);
+    m->streams.clear(); m->sbuf.clear(); m->gbuf.clear();
+    m->depth = 0;
+}
+}  // namespace
 
 void free_multi(rt_scene* s) {
     MultiDev* m = s->multi;
     if (!m) return;
     s->multi = nullptr;
+    free_multi_slots(m);
     Rccl* R = rccl(nullptr);
-    for (size_t i = 0; i < m->devices.size(); i++) {
+    for (size_t i = 0; i < m->comms.size(); i++) {
         (void)hipSetDevice(m->devices[i]);
-        if (i < m->streams.size() && m->streams[i]) { (void)hipStreamSynchronize(m->streams[i]); (void)hipStreamDestroy(m->streams[i]); }
-        if (i < m->sbuf.size() && m->sbuf[i]) (void)hipFree(m->sbuf[i]);
-        if (R && i < m->comms.size() && m->comms[i]) (void)R->comm_destroy(m->comms[i]);
+        if (R && m->comms[i]) (void)R->comm_destroy(m->comms[i]);
     }
-    if (m->gbuf) { (void)hipSetDevice(m->devices[0]); (void)hipFree(m->gbuf); }
+    (void)hipSetDevice(m->devices[0]);
+    if (m->ev_in) (void)hipEventDestroy(m->ev_in);
+    if (m->ev_out) (void)hipEventDestroy(m->ev_out);
     for (size_t i = 1; i < m->reps.size(); i++) delete m->reps[i];
     if (s->uploaded) (void)hipSetDevice(s->device);
     delete m;
@@ -2886,6 +2913,7 @@ void sync_replica(rt_scene* s, MultiDev* m, size_t i) {
     rt_scene* r = m->reps[i];
     r->h.cam = s->h.cam; r->h.d_cam = s->h.d_cam;
     r->h.dist_atten = s->h.dist_atten; r->h.ambience = s->h.ambience; r->h.depth = s->h.depth;
+    r->overlap = s->overlap;
     if (m->inst_gen[i] != s->inst_gen) {
         r->h.insts = s->h.insts; r->h.d_insts = s->h.d_insts;
         r->inst_gen++;
@@ -2898,6 +2926,57 @@ void sync_replica(rt_scene* s, MultiDev* m, size_t i) {
     }
 }
 
+// Replicas and communicators on first use; per-slot streams and buffers whenever the frame
+// slots changed (the work in flight is waited for first).
+int setup_multi(rt_scene* s, MultiDev* m, Rccl* R) {
+    const int nd = (int)m->devices.size(), W = m->W;
+    int r;
+    for (int i = (int)m->reps.size(); i < nd; i++) {
+        HIPCHK(hipSetDevice(m->devices[i]));
+        rt_scene* rp = new rt_scene;
+        rp->h = s->h; rp->finished = true;
+        rp->h.atlas_rgba.clear();
+        rp->overlap = s->overlap;
+        m->reps.push_back(rp);
+        m->inst_gen.push_back(0);
+        const int saved = g_device;
+        g_device = m->devices[i];
+        r = upload(rp);
+        g_device = saved;
+        if (r != RT_OK) return r;
+    }
+    if (m->comms.empty()) {
+        m->comms.assign(nd, nullptr);
+        ncclResult_t e = R->comm_init_all(m->comms.data(), nd, m->devices.data());
+        if (e != ncclSuccess) { m->comms.clear(); return fail(RT_ERR_HIP, std::string("ncclCommInitAll: ") + R->err(e)); }
+    }
+    HIPCHK(hipSetDevice(m->devices[0]));
+    if (!m->ev_in) HIPCHK(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
+    if (!m->ev_out) HIPCHK(hipEventCreateWithFlags(&m->ev_out, hipEventDisableTiming));
+    const int D = s->n_slots;
+    if (m->depth == D) return RT_OK;
+    free_multi_slots(m);
+    for (int i = 1; i < nd; i++) {                             // replicas rotate as many frame slots
+        m->reps[i]->overlap = s->overlap;
+        if ((r = rt_scene_set_frame_slots(m->reps[i], D)) != RT_OK) return r;
+    }
+    m->streams.assign(nd, std::vector<hipStream_t>(D, nullptr));
+    m->sbuf.assign(nd, std::vector<uint32_t*>(D, nullptr));
+    m->gbuf.assign(D, nullptr);
+    for (int i = 0; i < nd; i++) {
+        HIPCHK(hipSetDevice(m->devices[i]));
+        for (int k = 0; k < D; k++) {
+            HIPCHK(hipStreamCreateWithFlags(&m->streams[i][k], hipStreamNonBlocking));
+            HIPCHK(hipMalloc((void**)&m->sbuf[i][k], (size_t)m->per_dev * m->rows_max * W * 4));
+        }
+    }
+    HIPCHK(hipSetDevice(m->devices[0]));
+    for (int k = 0; k < D; k++) HIPCHK(hipMalloc((void**)&m->gbuf[k], (size_t)m->n_ranks * m->rows_max * W * 4));
+    m->depth = D;
+    m->frame = 0;
+    return RT_OK;
+}
+
 int render_multi(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     MultiDev* m = s->multi;
     if (o->radiance || o->hit_inst || o->hit_tri) return fail(RT_ERR_ARG, "multi-device frames write RGBA8 only");
@@ -2907,82 +2986,67 @@ int render_multi(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     const int nd = (int)m->devices.size(), N = m->n_ranks, W = s->h.cam.W, H = s->h.cam.H;
     int r;
     if (m->W != W || m->H != H) return fail(RT_ERR_STATE, "canvas size changed after rt_scene_set_devices");
-    // replicas, streams, buffers and communicators on first use
-    if (m->comms.empty()) {
-        for (int i = 0; i < nd; i++) {
-            HIPCHK(hipSetDevice(m->devices[i]));
-            if (i > 0) {
-                rt_scene* rp = new rt_scene;
-                rp->h = s->h; rp->finished = true;
-                rp->h.atlas_rgba.clear();
-                m->reps.push_back(rp);
-                m->inst_gen.push_back(0);
-                const int saved = g_device;
-                g_device = m->devices[i];
-                r = upload(rp);
-                g_device = saved;
-                if (r != RT_OK) return r;
-            }
-            hipStream_t st;
-            HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-            m->streams.push_back(st);
-            uint32_t* b = nullptr;
-            HIPCHK(hipMalloc((void**)&b, (size_t)m->per_dev * m->rows_max * W * 4));
-            m->sbuf.push_back(b);
-        }
-        HIPCHK(hipSetDevice(m->devices[0]));
-        HIPCHK(hipMalloc((void**)&m->gbuf, (size_t)N * m->rows_max * W * 4));
-        m->comms.assign(nd, nullptr);
-        ncclResult_t e = R->comm_init_all(m->comms.data(), nd, m->devices.data());
-        if (e != ncclSuccess) { m->comms.clear(); return fail(RT_ERR_HIP, std::string("ncclCommInitAll: ") + R->err(e)); }
-    }
+    if ((r = setup_multi(s, m, R)) != RT_OK) return r;
     for (int i = 1; i < nd; i++) sync_replica(s, m, i);
+    const int k = (int)(m->frame % m->depth);
+    hipStream_t caller = o->stream ? (hipStream_t)o->stream : nullptr;
+    if (caller) {                                          // the caller's work before this frame (its output buffer)
+        HIPCHK(hipSetDevice(m->devices[0]));
+        HIPCHK(hipEventRecord(m->ev_in, caller));
+    }
     unsigned long long tot[4] = {0, 0, 0, 0};
     double bvh_ms = 0, trace_ms = 0;
-    // 1. every rank's slice, on its device's stream
-    for (int i = 0; i < nd; i++)
+    // 1. every rank's slice, on its device's stream of this slot.  Event timing (o->timing)
+    // covers the first device's ranks (the scene's own rt_timing_collect); replicas untimed.
+    for (int i = 0; i < nd; i++) {
+        double dev_bvh = 0, dev_trace = 0;
         for (int j = 0; j < m->per_dev; j++) {
             rt_render_opts so = *o;
             so.row0 = i * m->per_dev + j; so.row_step = N; so.compact = 1;
-            so.rgba = m->sbuf[i] + (size_t)j * m->rows_max * W;
-            so.stream = m->streams[i]; so.host_outputs = 0; so.sync = 0;
+            so.rgba = m->sbuf[i][k] + (size_t)j * m->rows_max * W;
+            so.stream = m->streams[i][k]; so.host_outputs = 0; so.sync = 0;
+            if (i > 0) so.timing = 0;
             rt_stats st{};
             if ((r = rt_render(m->reps[i], &so, stats ? &st : nullptr)) != RT_OK) return r;
             if (stats) {
                 tot[0] += st.rays; tot[1] += st.nodes; tot[2] += st.leaves; tot[3] += st.tri_tests;
-                bvh_ms = std::max(bvh_ms, st.bvh_ms); trace_ms += st.trace_ms;
+                dev_bvh += st.bvh_ms; dev_trace += st.trace_ms;
             }
         }
+        bvh_ms = std::max(bvh_ms, dev_bvh); trace_ms = std::max(trace_ms, dev_trace);
+    }
     // 2. the gather to device 0 (one communicator per device, grouped)
     const size_t cnt = (size_t)m->per_dev * m->rows_max * W;
     ncclResult_t e = R->group_start();
     for (int i = 0; i < nd && e == ncclSuccess; i++) {
         HIPCHK(hipSetDevice(m->devices[i]));
-        e = R->gather(m->sbuf[i], i == 0 ? m->gbuf : nullptr, cnt, ncclUint32, 0, m->comms[i], m->streams[i]);
+        e = R->gather(m->sbuf[i][k], i == 0 ? m->gbuf[k] : nullptr, cnt, ncclUint32, 0, m->comms[i], m->streams[i][k]);
     }
     ncclResult_t e2 = R->group_end();
     if (e == ncclSuccess) e = e2;
     if (e != ncclSuccess) return fail(RT_ERR_HIP, std::string("ncclGather: ") + R->err(e));
-    // 3. un-permute on device 0 into the caller's buffer or the canvas
+    // 3. un-permute on device 0 into the caller's buffer (after the caller's earlier work on it)
+    // or the canvas
     HIPCHK(hipSetDevice(m->devices[0]));
+    hipStream_t s0 = m->streams[0][k];
+    if (caller) HIPCHK(hipStreamWaitEvent(s0, m->ev_in, 0));
     uint32_t* out = (o->rgba && !o->host_outputs) ? o->rgba : s->d_canvas;
     const long long px = (long long)W * H;
-    hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, m->streams[0], m->gbuf, out, W, H,
-                       N, m->rows_max);
+    hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((px + 255) / 256)), dim3(256), 0, s0, m->gbuf[k], out, W, H, N,
+                       m->rows_max);
     HIPCHK(hipGetLastError());
-    hipStream_t caller = o->stream ? (hipStream_t)o->stream : nullptr;
     if (caller) {                                          // the caller's stream continues after the frame
-        hipEvent_t ev;
-        HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ev, m->streams[0]));
-        HIPCHK(hipStreamWaitEvent(caller, ev, 0));
-        HIPCHK(hipEventDestroy(ev));
+        HIPCHK(hipEventRecord(m->ev_out, s0));
+        HIPCHK(hipStreamWaitEvent(caller, m->ev_out, 0));
     }
-    if (o->sync || o->host_outputs || stats)
-        for (int i = 0; i < nd; i++) { HIPCHK(hipSetDevice(m->devices[i])); HIPCHK(hipStreamSynchronize(m->streams[i])); }
+    m->frame++;
+    if (o->sync || o->host_outputs || stats)               // this frame only: the other slots keep running
+        for (int i = 0; i < nd; i++) { HIPCHK(hipSetDevice(m->devices[i])); HIPCHK(hipStreamSynchronize(m->streams[i][k])); }
     HIPCHK(hipSetDevice(m->devices[0]));
     if (o->host_outputs && o->rgba) HIPCHK(hipMemcpy(o->rgba, out, (size_t)px * 4, hipMemcpyDeviceToHost));
     if (stats) {
+        // counters summed over ranks; bvh_ms / trace_ms: the slowest device's summed kernel times
+        // (its ranks run one after another on its stream), the frame's parallel kernel time
         stats->rays = tot[0]; stats->nodes = tot[1]; stats->leaves = tot[2]; stats->tri_tests = tot[3];
         stats->bvh_ms = bvh_ms; stats->trace_ms = trace_ms;
     }

@@ -63,8 +63,10 @@ def test_cpp_shim_and_cli_compile_against_the_abi(tmp_path):
     libdir = os.path.join(ROOT, "gpu-ray-tracer_amd")
     for src in (os.path.join(ROOT, "tests", "shim_world.cpp"), os.path.join(ROOT, "tests", "shim_main.cpp"),
                 os.path.join(libdir, "cli", "rtracer.cpp")):
+        hip = ["-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lamdhip64"] \
+            if src.endswith("rtracer.cpp") else []
         r = subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", inc, src, "-o", str(tmp_path / "a.out"),
-                            "-L", libdir, "-lrt_amd"], capture_output=True, text=True)
+                            "-L", libdir, "-lrt_amd"] + hip, capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
 
 

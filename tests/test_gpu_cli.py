@@ -152,3 +152,20 @@ def test_cpp_shim_main_cc_calls(oracle, tmp_path):
     exp = oracle.render(o, spp=1, nthreads=8, want=("rgba",))["rgba"]
     assert np.array_equal(frame, exp)
     assert (frame != 0).any()
+
+
+@pytest.mark.parametrize("extra", [["--in-flight", "4"], ["--gpus", "1", "--ranks", "8", "--in-flight", "8"]])
+def test_cli_frames_in_flight(oracle, tmp_path, extra):
+    """--in-flight D: frames issued asynchronously, D in flight, each into its own device buffer on
+    its own stream (single device, and 8 row-cyclic slices through rt_scene_set_devices with one
+    slot's streams per frame); the last frame equals the oracle's."""
+    out = str(tmp_path / "p.ppm")
+    r = _run([CLI, "-c", scene_path("world8_stress"), "--width", "240", "--height", "136", "--spp", "2",
+              "--frames", "12", "--out", out] + extra)
+    assert r.returncode == 0, r.stderr
+    assert "ms/frame" in r.stdout
+    o = oracle.render(oracle.load(scene_path("world8_stress"), 240, 136), spp=2, nthreads=8, want=("rgba",))
+    rgba = o["rgba"]
+    exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
+    got = _ppm_rgb(out)
+    assert np.abs(got.astype(int) - exp.astype(int)).max() <= 1 and (got != exp).mean() < 1e-3
