@@ -2870,6 +2870,10 @@ struct MultiDev {
     std::vector<std::vector<uint32_t*>> sbuf;        // [device][slot]: per_dev slices of rows_max x W
     std::vector<uint32_t*> gbuf;                     // [slot], device 0: n_ranks slices
     hipEvent_t ev_in = nullptr, ev_out = nullptr;    // device 0: caller's stream -> frame -> caller's stream
+    // per device: the last frame's gather; the next frame's gather (another slot's stream) waits
+    // for it, so operations on a communicator run in issue order whatever RCCL does across streams
+    std::vector<hipEvent_t> gdone;
+    bool gdone_pending = false;
 };
 
 namespace {
@@ -2897,6 +2901,10 @@ void free_multi(rt_scene* s) {
     for (size_t i = 0; i < m->comms.size(); i++) {
         (void)hipSetDevice(m->devices[i]);
         if (R && m->comms[i]) (void)R->comm_destroy(m->comms[i]);
+    }
+    for (size_t i = 0; i < m->gdone.size(); i++) {
+        (void)hipSetDevice(m->devices[i]);
+        if (m->gdone[i]) (void)hipEventDestroy(m->gdone[i]);
     }
     (void)hipSetDevice(m->devices[0]);
     if (m->ev_in) (void)hipEventDestroy(m->ev_in);
@@ -2945,6 +2953,13 @@ int setup_multi(rt_scene* s, MultiDev* m, Rccl* R) {
         g_device = saved;
         if (r != RT_OK) return r;
     }
+    if (m->gdone.empty()) {
+        m->gdone.assign(nd, nullptr);
+        for (int i = 0; i < nd; i++) {
+            HIPCHK(hipSetDevice(m->devices[i]));
+            HIPCHK(hipEventCreateWithFlags(&m->gdone[i], hipEventDisableTiming));
+        }
+    }
     if (m->comms.empty()) {
         m->comms.assign(nd, nullptr);
         ncclResult_t e = R->comm_init_all(m->comms.data(), nd, m->devices.data());
@@ -2974,6 +2989,7 @@ int setup_multi(rt_scene* s, MultiDev* m, Rccl* R) {
     for (int k = 0; k < D; k++) HIPCHK(hipMalloc((void**)&m->gbuf[k], (size_t)m->n_ranks * m->rows_max * W * 4));
     m->depth = D;
     m->frame = 0;
+    m->gdone_pending = false;
     return RT_OK;
 }
 
@@ -3017,6 +3033,11 @@ int render_multi(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     }
     // 2. the gather to device 0 (one communicator per device, grouped)
     const size_t cnt = (size_t)m->per_dev * m->rows_max * W;
+    if (m->gdone_pending)                                  // after the previous frame's gather (issue order)
+        for (int i = 0; i < nd; i++) {
+            HIPCHK(hipSetDevice(m->devices[i]));
+            HIPCHK(hipStreamWaitEvent(m->streams[i][k], m->gdone[i], 0));
+        }
     ncclResult_t e = R->group_start();
     for (int i = 0; i < nd && e == ncclSuccess; i++) {
         HIPCHK(hipSetDevice(m->devices[i]));
@@ -3025,6 +3046,11 @@ int render_multi(rt_scene* s, const rt_render_opts* o, rt_stats* stats) {
     ncclResult_t e2 = R->group_end();
     if (e == ncclSuccess) e = e2;
     if (e != ncclSuccess) return fail(RT_ERR_HIP, std::string("ncclGather: ") + R->err(e));
+    for (int i = 0; i < nd; i++) {
+        HIPCHK(hipSetDevice(m->devices[i]));
+        HIPCHK(hipEventRecord(m->gdone[i], m->streams[i][k]));
+    }
+    m->gdone_pending = true;
     // 3. un-permute on device 0 into the caller's buffer (after the caller's earlier work on it)
     // or the canvas
     HIPCHK(hipSetDevice(m->devices[0]));

@@ -6,6 +6,10 @@ k-ordered sum, truncating RGBA8):
   renders it -- eight frame slots, frames on rotating streams (FramePipeline), fast kernels with
   the sky pre-pass -- on one GPU, and as 2 / 8 row-cyclic rank slices reassembled;
 - config 3: world8 1920x1080 8 spp; config 2: world1 1920x1080 brute force (counters too);
+- config 5 at its own size: world16 and world16_tex (textured mode) at 3840x2160, 64 spp, the
+  fast frame (pipelined as bench.py renders it, and with every output) against the oracle on
+  every 45th row, and the counted kernel on the same rows (fast == counted bit for bit, counters
+  equal the oracle's);
 - config 5's sample mapping at a reduced size: world16 and world16_tex (textured mode) at
   320x180 with spp = 64 (64 lanes per pixel, one pixel per wave, 1x1 sky cones, the generic
   reduction) and spp = 96 (the M_MULTI rounds), fast and counted kernels.
@@ -29,12 +33,15 @@ def stress_1080p(oracle):
     return oracle.render(oracle.load(scene_path("world8_stress"), W, H), spp=8, nthreads=NTHREADS)
 
 
-def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=False):
+def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=False, size=(W, H)):
     """This rank's rows of the last of n_frames frames issued as bench.py issues them."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
     import rtamd.dist as rtdist
+    W, H = size
     s = gpu.Scene.load_json(scene_path(scene), W, H)
+    if textures:
+        s.load_atlas()
     s.set_frame_slots(depth)
     pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", depth=depth)
     for k in range(n_frames):
@@ -112,3 +119,33 @@ def test_config5_sample_mapping(gpu, oracle, scene, textures, spp):
     for k in WANT:
         assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
     assert (full["hit_inst"] >= 0).mean() > 0.2
+
+
+@pytest.mark.parametrize("scene,textures", [("world16", False), ("world16_tex", True)])
+def test_config5_full_size(gpu, oracle, scene, textures):
+    """Config 5 (BASELINE.json: world16, 3840x2160, 64 spp, textured) at its own size.  The fast
+    frame -- the unparked ordered-tree kernel world16's 93 KB tree leaves room for -- rendered as
+    bench.py renders it (eight frame slots, rotating streams) and once with every output; rows
+    y % 45 == 0 (48 rows, 11.8 M samples) against the oracle; the counted kernel on the same rows
+    equals the fast frame bit for bit and its counters equal the oracle's."""
+    w, h, spp, step = 3840, 2160, 64, 45
+    s = gpu.Scene.load_json(scene_path(scene), w, h)
+    o = oracle.load(scene_path(scene), w, h)
+    if textures:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import make_atlas
+        s.load_atlas()
+        o.set_atlas(make_atlas.atlas())
+        o.set_textures(True)
+    piped = _pipelined(gpu, scene, spp, n_frames=9, textures=textures, size=(w, h))
+    fast = s.render(spp=spp, want=WANT, stats=False, textures=textures)
+    assert np.array_equal(piped, fast["rgba"])
+    rows = slice(0, None, step)
+    of = oracle.render(o, spp=spp, row0=0, row_step=step, nthreads=NTHREADS)
+    assert_frames_equal({k: fast[k][rows] for k in WANT}, {k: of[k][rows] for k in WANT}, ctx=scene)
+    counted = s.render(spp=spp, row0=0, row_step=step, compact=True, want=WANT, stats=True, textures=textures)
+    for k in WANT:
+        assert np.array_equal(counted[k].view(np.uint32), fast[k][rows].view(np.uint32)), k
+    st = counted["stats"]
+    assert (st["rays"], st["nodes"], st["leaves"], st["tri_tests"]) == tuple(int(x) for x in of["stats"])
+    assert (fast["hit_inst"] >= 0).mean() > 0.2
