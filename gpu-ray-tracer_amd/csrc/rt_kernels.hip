@@ -799,6 +799,26 @@ __device__ __forceinline__ KTP& kparams() {
     asm volatile("" : "+s"(p));
     return *p;
 }
+// The trace kernel's SceneView (its second argument, right after TraceParams) read the same way:
+// a fresh copy per scope (the state loop's iteration, the group) is loaded where it is used
+// instead of being held in SGPRs across the persistent loops.  RT_FRESH_SCENE=0: the by-value
+// argument throughout (the A/B arm).
+#ifndef RT_FRESH_SCENE
+#define RT_FRESH_SCENE 1
+#endif
+typedef __attribute__((address_space(4))) const SceneView KSV;
+static_assert(sizeof(TraceParams) % alignof(SceneView) == 0, "SceneView follows TraceParams in the kernarg segment");
+__device__ __forceinline__ SceneView kscene() {
+    const __attribute__((address_space(4))) char* p =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return kld(*(KSV*)(p + sizeof(TraceParams)));
+}
+#if RT_FRESH_SCENE
+#define SV() kscene()
+#else
+#define SV() S
+#endif
 
 // Textured mode (build-defined; phong.cu:18-23 leaves texture mapping a TODO): the
 // diffuse colour of a hit on a triangle with TextureCoords is the atlas texel at
@@ -921,7 +941,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
             if (st == ST_LIGHT) {
-                if (li < S.n_lights) {
+                if (li < SV().n_lights) {
                     const DLight L = bv.lights[li];
                     const V3 hpos = at(cur.ray, is_time);          // org_ray.at(isect.time) (phong.cu:48)
                     V3 dtl;
@@ -1040,7 +1060,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         // (an unlit-skipped shadow step, max_t = -inf, takes no query)
         const bool qa = st == ST_WAIT_NORMAL || (st == ST_WAIT_SHADOW && max_t >= 0.0f);
         const unsigned long long prof_p0 = wc.wpair, prof_l0 = wc.wleaf;
-        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(S, bv, qa, q, b, wc, occl, lim);
+        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(SV(), bv, qa, q, b, wc, occl, lim);
         if (PROF && P.stats) {                                 // query occupancy (rt_frame_work)
             const unsigned long long mp = __ballot(st == ST_WAIT_NORMAL && (fl & 1));
             const unsigned long long mn = __ballot(st == ST_WAIT_NORMAL);
@@ -1083,7 +1103,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         V3 hn = v3(0, 0, 0);
         // (opaque scenes: a shadow segment needs neither the normal nor the material -- any hit
         // before the light is opaque, light.cu:44-46)
-        if (hit && (!OPQ || st == ST_WAIT_NORMAL)) hn = hit_normal(S, bv, b, hmat);
+        if (hit && (!OPQ || st == ST_WAIT_NORMAL)) hn = hit_normal(SV(), bv, b, hmat);
         if (st == ST_WAIT_NORMAL) {
             if (fl & 1) {
                 fl &= ~1;
@@ -1372,7 +1392,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // tree's root -- the traversal's first step, same test -- every sample misses, its
             // radiance is the integrator's initial zero (scene.cu:124-126) and the group's
             // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
-            if (FT && !STATS && !PROF && !MULTI && S.use_bvh && S.n_leaf > 0 && !kparams().gsky && !__ballot(ft_root_hit(S, bv, act, r0))) {
+            if (FT && !STATS && !PROF && !MULTI && SV().use_bvh && SV().n_leaf > 0 && !kparams().gsky && !__ballot(ft_root_hit(SV(), bv, act, r0))) {
                 if (act && k == 0) {
                     int op = pix_index;
                     opaque(op);
@@ -1383,7 +1403,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             }
             // PROF: the group is live when some primary enters the tree's root (the sky pre-pass's
             // test); occupancy counters are taken over live groups' queries only
-            if (PROF && FT) wc.live = __ballot(ft_root_hit(S, bv, act, r0)) != 0;
+            if (PROF && FT) wc.live = __ballot(ft_root_hit(SV(), bv, act, r0)) != 0;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
             V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
                                                  park);

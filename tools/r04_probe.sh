@@ -9,3 +9,5 @@ for a in "--gpus 1 --ranks 8 --in-flight 8" "--gpus 1 --ranks 8 --in-flight 4" "
   timeout -k 10 120 ./gpu-ray-tracer_amd/rtracer -c scenes/world8_stress.json --width 1920 --height 1080 --spp 8 --frames 40 $a >> gpurun_out/r04/cli_inflight.log 2>&1 || exit 1
 done
 timeout -k 10 300 python3 bench.py --scene world16 --width 3840 --height 2160 --spp 64 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r04/bench_w16.log 2>&1
+# A/B: scene view read in place at use sites (RT_FRESH_SCENE=1, librt_amd.so) vs the by-value argument
+bash tools/ab_libs.sh r04/ab_fresh 3 0 gpu-ray-tracer_amd/librt_fs0.so gpu-ray-tracer_amd/librt_amd.so > gpurun_out/r04/ab_fresh.log 2>&1
