@@ -67,8 +67,10 @@ constexpr int PARK_LDS_LIMIT = 158 * 1024;   // BVH image + parking area (160 KB
 #endif
 constexpr int NQ = RT_NQ;                    // work queues (one per XCD dispatch slot), 64-B apart
 // work counters: [16 q] queue q's tickets, [16 NQ] the heavy list's, [16 (NQ + 1 + q)] the
-// length of live-group list q (sky_kernel)
-constexpr int WORK_INTS = 16 * (2 * NQ + 1);
+// length of live-group list q (sky_kernel), [16 (2 NQ + 1)] the length of this frame's heavy
+// live list (hist = 2)
+constexpr int WORK_INTS = 16 * (2 * NQ + 2);
+constexpr int WORK_HEAVY_LEN = 16 * (2 * NQ + 1);
 // Statistics / profiling counters (d_stats): [0, 22) rt_stats and the PROF step counts and
 // cycle split (rt_experiment), [22, 24) spare, [24, 64) the PROF variant's query-occupancy
 // counters (PROF_* below, rt_frame_work).
@@ -194,6 +196,9 @@ struct BvhRefs {
 // Tuning parameters (build switches; the A/B logs under profiles/ record the values tried).
 #ifndef RT_HIST_GROUPS_PER_WAVE
 #define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
+#endif
+#ifndef RT_HEAVY_Q_DEFAULT
+#define RT_HEAVY_Q_DEFAULT 6        // hist = 2: a group of >= this many wave queries is heavy
 #endif
 #ifndef RT_TPC
 #define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop) over all
@@ -756,6 +761,10 @@ struct TraceParams {
     // (hf_prev); this frame records its own into the *_next buffers.  hs_* = summed group
     // durations (100 MHz ticks) for the threshold (4x the mean group).
     int hist, heavy_cap;      // heavy_cap: most heavy groups recorded per frame
+    // hist = 2 (whole frames with the sky pre-pass): heavy = a group that took >= heavy_q wave
+    // queries (counted, no clock); hf_next[g] = 1 records it, and the next frame's sky pre-pass
+    // puts the groups flagged in hf_prev on a heavy live list the trace kernel drains first
+    int heavy_q;
     const int* hl_prev; int* hl_next;
     const unsigned char* hf_prev; unsigned char* hf_next;
     const unsigned long long* hctl_prev; unsigned long long* hctl_next;   // {count, sum}
@@ -905,7 +914,7 @@ constexpr int PARK_FIELDS = 26;
 __host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 22 : PARK_FIELDS; }
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
-                                           Ray r0, bool me, int out_p, WaveCounters& wc, float* park) {
+                                           Ray r0, bool me, int out_p, WaveCounters& wc, float* park, int& nq) {
     constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
     KTP& P0 = kparams();
     Frame cur;
@@ -1039,6 +1048,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         // ---- the wave-collective closest-hit query ----
         const bool need = (st == ST_WAIT_NORMAL || st == ST_WAIT_SHADOW);
         if (!__ballot(need)) break;
+        nq++;                                                  // a wave query (uniform)
         Best b;
         b.time = INFINITY; b.inst = -1; b.tri = -1; b.u = 0.0f; b.v = 0.0f;
         float occl = -1.0f;
@@ -1282,7 +1292,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     const int per_q = (P.n_groups + NQ - 1) / NQ;
     int n_heavy = 0;
     unsigned long long thr = ~0ull, wave_sum = 0;
-    if (P.hist) {
+    if (P.hist == 2) {
+        n_heavy = ldc(P.work, WORK_HEAVY_LEN);                 // this frame's heavy live list (sky_kernel)
+    } else if (P.hist) {
         n_heavy = (int)min(P.hctl_prev[0], (unsigned long long)P.heavy_cap);
         // heavy: over 4x the previous frame's mean group and over 20 us (2000 ticks of the 100 MHz
         // clock) -- in a frame of uniformly cheap groups the mean-relative test alone flags
@@ -1304,6 +1316,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     // raster order, where expensive regions cluster); indices >= n are skipped
     auto live_n = [&](int q) { return ldc(kparams().work, 16 * (NQ + 1 + (q0 + q) % NQ)); };
     auto live_span = [&](int q) { const int n = live_n(q); return n <= 1 ? n : 1 << (32 - __builtin_clz((unsigned)n - 1)); };
+    auto pow2_span = [](int n) { return n <= 1 ? n : 1 << (32 - __builtin_clz((unsigned)n - 1)); };
     auto request = [&](int q) {
         KTP& Pq = kparams();
         // The address goes through a VGPR so the atomic optimizer leaves the atomic alone:
@@ -1324,7 +1337,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         KTP& P = kparams();                                    // this group's reads of the launch parameters
         for (;;) {                                             // next work index tbase + j of queue qi
             if (qi >= NQ) break;
-            const int lim = qi < 0 ? n_heavy : kparams().live ? live_span(qi) : per_q;
+            const int lim = qi < 0 ? (kparams().hist == 2 ? pow2_span(n_heavy) : n_heavy) : kparams().live ? live_span(qi) : per_q;
             if (tbase + j >= lim) {                             // queue drained (a pending batch is past it too)
                 if (inflight) (void)resolve();
                 qi++; j = 0;
@@ -1350,15 +1363,20 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             const int i = (int)(((unsigned)ticket * 0x9E3779B1u) & (unsigned)(live_span(qi) - 1));
             return i < n ? ldc(P.live, ((q0 + qi) % NQ) * P.live_cap + i) : P.n_groups;
         };
-        const int g = qi < 0 ? ldc(P.hl_prev, ticket)
+        auto heavy_g = [&]() {                                 // hist = 2: the heavy live list, scrambled
+            const int i = (int)(((unsigned)ticket * 0x9E3779B1u) & (unsigned)(pow2_span(n_heavy) - 1));
+            return i < n_heavy ? ldc(P.live, NQ * P.live_cap + i) : P.n_groups;
+        };
+        const int g = qi < 0 ? (P.hist == 2 ? heavy_g() : ldc(P.hl_prev, ticket))
                              : P.live ? live_g()
                              : ((q0 + qi) % NQ) + NQ * (P.scramble_small ? (int)umod((unsigned)ticket * (unsigned)P.scramble)
                                                                          : (int)(((long long)ticket * P.scramble) % per_q));
         auto flag = [&](const unsigned char* f) { return (ldc(reinterpret_cast<const uint32_t*>(f), g >> 2) >> (8 * (g & 3))) & 0xffu; };
-        if (g >= P.n_groups || (qi < 0 && P.gsky && flag(P.gsky)) ||    // sky group: done by sky_kernel
-            (qi >= 0 && P.hist && flag(P.hf_prev)))
+        if (g >= P.n_groups || (qi < 0 && P.hist == 1 && P.gsky && flag(P.gsky)) ||    // sky group: done by sky_kernel
+            (qi >= 0 && P.hist == 1 && flag(P.hf_prev)))
             continue;
-        const unsigned long long g_start = P.hist ? __builtin_amdgcn_s_memrealtime() : 0;
+        const unsigned long long g_start = P.hist == 1 ? __builtin_amdgcn_s_memrealtime() : 0;
+        int nq = 0;                                            // wave queries of this group (hist = 2)
         const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
         // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
         // kept live across the trace
@@ -1406,7 +1424,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             if (PROF && FT) wc.live = __ballot(ft_root_hit(SV(), bv, act, r0)) != 0;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
             V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
-                                                 park);
+                                                 park, nq);
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
                 return v4(v.x > 1.0f ? 1.0f : v.x, v.y > 1.0f ? 1.0f : v.y, v.z > 1.0f ? 1.0f : v.z, v.w > 1.0f ? 1.0f : v.w);
@@ -1470,7 +1488,10 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
             atomicMax(&P.stats[21], wc.wq - g_q0);
         }
-        if (kparams().hist) {                 // record for the next frame's order
+        if (kparams().hist == 2) {            // heavy by work: the next frame's pre-pass runs it first
+            KTP& P = kparams();
+            if (nq >= P.heavy_q && lane_id_fresh() == 0) P.hf_next[g] = 1;
+        } else if (kparams().hist) {          // record for the next frame's order
             KTP& P = kparams();
             const unsigned long long dur = __builtin_amdgcn_s_memrealtime() - g_start;   // wave-uniform (scalar)
             const bool heavy = dur > thr;
@@ -1497,7 +1518,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             }
         }
     }
-    if (P.hist && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
+    if (P.hist == 1 && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
     if (CYC && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
         if (wc.nodes) atomicAdd(&P.stats[1], wc.nodes);
@@ -1604,9 +1625,12 @@ __device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const Sce
 #define RT_SKY_WAVES 4       // waves per sky_kernel block (64 groups per block)
 #endif
 constexpr int SKY_THREADS = 64 * RT_SKY_WAVES;
+static_assert(SKY_THREADS >= 128, "sky_kernel's heavy-list append uses threads 64..127");
 __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
     __shared__ unsigned long long s_sky, s_todo;
     __shared__ int s_cnt, s_base, s_list[64];
+    __shared__ int s_hcnt, s_hbase, s_hlist[64];               // hist = 2: last frame's heavy groups
+    const bool h2 = P.hist == 2;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, L = P.lanes_per_px;
     const int base = blockIdx.x * 64;
     const int n_in = min(64, P.n_groups - base);
@@ -1632,18 +1656,26 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
             gsky[gl] = 1;
             // the trace kernel records (hf_next) only the groups it runs: a sky group's entry
             // must not keep a heavy flag from the frame that last wrote this buffer
-            if (P.hist) P.hf_next[gl] = 0;
+            if (P.hist == 1) P.hf_next[gl] = 0;
         }
-        if (lane == 0) { s_sky = m; s_todo = t; s_cnt = 0; }
+        if (lane == 0) { s_sky = m; s_todo = t; s_cnt = 0; s_hcnt = 0; }
         if (rlive) gsky[gl] = 0;
-        const unsigned long long rl = __ballot(rlive);
+        // hist = 2: a live group the previous frame found heavy goes on the heavy list instead
+        const bool hv = rlive && h2 && P.hf_prev[gl];
+        const unsigned long long rl = __ballot(rlive && !hv), hl = __ballot(hv);
         if (rl) {                                              // live already: into the block's list
             const int pos = __popcll(rl & ((1ull << lane) - 1ull));
-            if (rlive) s_list[pos] = gl;
+            if (rlive && !hv) s_list[pos] = gl;
             if (lane == 0) s_cnt = __popcll(rl);
+        }
+        if (hl) {
+            const int pos = __popcll(hl & ((1ull << lane) - 1ull));
+            if (hv) s_hlist[pos] = gl;
+            if (lane == 0) s_hcnt = __popcll(hl);
         }
     }
     __syncthreads();
+    if (h2 && (int)threadIdx.x < n_in) P.hf_next[base + threadIdx.x] = 0;   // this frame records afresh
     auto sky_pixel = [&](int g, int pix) {                     // pixel pix of sky group g: zeros, -1 hit ids
         const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
         const int qx = P.gw_shift >= 0 ? pix & (P.gw - 1) : pix % P.gw;
@@ -1689,17 +1721,23 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
         const bool sky = __ballot(ft_root_hit(S, bv, act, r0)) == 0;
         if (lane == 0) {
             gsky[g] = sky ? 1 : 0;
-            if (sky && P.hist) P.hf_next[g] = 0;
-            if (!sky) s_list[atomicAdd(&s_cnt, 1)] = g;
+            if (sky && P.hist == 1) P.hf_next[g] = 0;
+            if (!sky) {
+                if (h2 && P.hf_prev[g]) s_hlist[atomicAdd(&s_hcnt, 1)] = g;
+                else s_list[atomicAdd(&s_cnt, 1)] = g;
+            }
         }
         if (sky && valid && sub_g == 0) sky_pixel(g, pix_g);
     }
     __syncthreads();
-    const int q = blockIdx.x % NQ, n = s_cnt;
-    if (n == 0) return;
-    if (threadIdx.x == 0) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], n);
+    const int q = blockIdx.x % NQ, n = s_cnt, nh = s_hcnt;
+    if (n == 0 && nh == 0) return;
+    if (threadIdx.x == 0 && n) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], n);
+    if (threadIdx.x == 64 && nh) s_hbase = atomicAdd(&P.work[WORK_HEAVY_LEN], nh);
     __syncthreads();
-    if (threadIdx.x < n) live[q * P.live_cap + s_base + threadIdx.x] = s_list[threadIdx.x];
+    if ((int)threadIdx.x < n) live[q * P.live_cap + s_base + threadIdx.x] = s_list[threadIdx.x];
+    if ((int)threadIdx.x >= 64 && (int)threadIdx.x < 64 + nh)            // heavy list after the NQ lists
+        live[NQ * P.live_cap + s_hbase + threadIdx.x - 64] = s_hlist[threadIdx.x - 64];
 }
 
 // ---------------------------------------------------------------------------
@@ -2713,24 +2751,33 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // 4-way 0.360 / 0.360, 8-way 0.179-0.186 / 0.200-0.204; profiles/r02/hist_policy.log).
     P.hist = 0;
     const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
-    if (!want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves)) {
+    // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
+    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
+    // Heavy-first by work (hist = 2) where groups per wave are many: a group whose samples took
+    // >= heavy_q wave queries (mirror pixels: primary, shadow and reflection chains) is flagged,
+    // and the next frame of the slot runs the flagged groups first off a heavy live list the sky
+    // pre-pass builds.  No clock reads (the timed history's cost, item 17), one byte store per
+    // heavy group.  RT_HEAVY_Q (environment) sets heavy_q; 0 turns it off.
+    static const int heavy_q = [] { const char* e = getenv("RT_HEAVY_Q"); return e ? atoi(e) : RT_HEAVY_Q_DEFAULT; }();
+    const bool hist1 = !want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves);
+    const bool hist2 = !hist1 && !want_stats && !dbg && sky && heavy_q > 0;
+    if (hist1 || hist2) {
         const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
         int r;
         const int cap0 = s->hist_cap;
         if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
         if (s->n_slots > 1 && s->hist_cap > cap0 && (r = mirror_slot_caps(s)) != RT_OK) return r;
         const int prev = s->hist_parity, next = 1 - prev;
-        P.hist = 1;
+        P.hist = hist1 ? 1 : 2;
+        P.heavy_q = heavy_q;
         P.hl_prev = s->d_hlist[prev]; P.hl_next = s->d_hlist[next];
         P.hf_prev = s->d_hflag[prev]; P.hf_next = s->d_hflag[next];
         P.hctl_prev = s->d_hctl + 2 * prev; P.hctl_next = s->d_hctl + 2 * next;
-        if (s->hctl_zeroed != next) HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
+        if (hist1 && s->hctl_zeroed != next) HIPCHK(hipMemsetAsync(s->d_hctl + 2 * next, 0, 2 * sizeof(unsigned long long), st));
         s->hist_parity = next;
     }
     s->work_zeroed = false;                                   // this launch consumes the counters
     s->hctl_zeroed = -1;
-    // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
-    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
     if (sky) {
         bool grew = false;
         if (P.n_groups > s->gsky_cap) {
@@ -2742,11 +2789,12 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         }
         const int sblocks = (P.n_groups + 63) / 64;
         const int lcap = (sblocks + NQ - 1) / NQ * 64;          // most groups of the blocks b = q mod NQ
-        if ((long long)lcap * NQ > s->live_cap) {
+        const int need = lcap * NQ + P.n_groups;                // + the heavy live list (hist = 2)
+        if (need > s->live_cap) {
             grew = true;
             dfree(s->d_live);
-            HIPCHK(hipMalloc((void**)&s->d_live, (size_t)lcap * NQ * sizeof(int)));
-            s->live_cap = lcap * NQ;
+            HIPCHK(hipMalloc((void**)&s->d_live, (size_t)need * sizeof(int)));
+            s->live_cap = need;
         }
         P.gsky = s->d_gsky;
         P.live = s->d_live; P.live_cap = lcap;
