@@ -4,22 +4,26 @@
 // (src/raytracer.cu:102-120) = per-frame BVH build + the per-pixel `trace`
 // megakernel running renv::gpu::propagate_ray (src/rayenv/scene.cu:92-188).
 //
-// MI355X design:
-//  * bvh_build: ONE workgroup of 1024 threads builds the whole Morton BVH
-//    (boxes -> 64-bit z-order keys -> LDS bitonic sort of (key, index) == the
-//    reference's stable thrust::sort_by_key -> pairwise level merges), replacing
-//    the reference's 6+ launches and its 1-thread top-level kernel (bvh.cu:64-73).
-//    Nodes are written in heap order (k = 1 .. 2n-1, children 2k / 2k+1) as
-//    32-byte records.
-//  * trace: one lane per pixel, wave = 8x8 pixel tile, block = 16x16.  Each
-//    lane runs the reference's frame-stack integrator as a state machine whose
-//    ONLY wave-collective step is a closest-hit query: every lane with a pending
-//    query (primary, reflection, refraction or shadow segment) traverses the BVH
-//    together.  Traversal is the reference's stackless heap walk made 64-wide:
-//    the node index is wave-uniform (SGPR), node and triangle records are read
-//    with scalar loads, `__ballot` decides descend vs. skip (scene.cu:54-70).
-//    Leaf and box tests use the reference's exact float32 operations, so hit
-//    indices are bit-identical to the single-ray semantics.
+// MI355X design (DESIGN.md §2-§3):
+//  * bvh_build_kernel: ONE workgroup of 1024 threads per frame builds the reference's Morton
+//    BVH (boxes -> 64-bit z-order keys -> an LDS rank sort equal to thrust's stable
+//    sort_by_key -> pairwise level merges, bvh.cu:11-91) in the reference's heap layout (child
+//    pairs as three float4) and, from the same sorted leaves, an ordered LBVH for the fast
+//    kernels (64-B records, leaves met in the heap's DFS order).  Above 8192 padded leaves the
+//    grid-wide build of rt_bvh_large.hip takes over.
+//  * sky_kernel: a pre-pass over pixel groups (8 pixels x 8 samples at 8 spp): a group none of
+//    whose primary rays enters the tree's root is written here (zeros, -1 hit ids) and the
+//    live groups go onto per-queue lists (and, hist = 2, the previous frame's heavy groups onto
+//    a heavy list run first).
+//  * trace_kernel: persistent 1024-thread blocks, one per CU, with the scene (ordered tree,
+//    instances, shading records) staged in LDS.  A wave takes live groups from work queues;
+//    lane = (pixel, sample).  Each lane runs propagate_ray (scene.cu:92-188) as a state machine
+//    whose only wave-collective step is the closest-hit query: a packet traversal with the node
+//    index wave-uniform (SGPR), 16-B broadcast LDS record reads, a filtered slab test with the
+//    exact reference test as fallback, and ballots for descend / push / pop.  Integrator state
+//    the traversal does not read is parked in LDS during the query.  Every filter and pruning
+//    is exact: hit ids equal the reference's single-ray semantics and
+//    radiance its float32 operations.
 #include <dlfcn.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
