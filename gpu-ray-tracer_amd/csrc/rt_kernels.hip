@@ -2762,11 +2762,18 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // and the next frame of the slot runs the flagged groups first off a heavy live list the sky
     // pre-pass builds.  No clock reads (the timed history's cost, item 17), one byte store per
     // heavy group.  RT_HEAVY_Q (environment) sets heavy_q; 0 turns it off.
+    // The mode must not depend on the grid (half or whole, frames in flight or alone): the two
+    // modes' flags mean different things (hist = 1 flags only the groups on its heavy list and
+    // skips them in the normal queues; hist = 2 flags by work and lists nothing), so the history
+    // key includes the mode and a change of mode resets the flags.
     static const int heavy_q = [] { const char* e = getenv("RT_HEAVY_Q"); return e ? atoi(e) : RT_HEAVY_Q_DEFAULT; }();
-    const bool hist1 = !want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * waves);
-    const bool hist2 = !hist1 && !want_stats && !dbg && sky && heavy_q > 0;
+    const long long full_waves = (long long)s->n_cu * per_cu * (TRACE_BLOCK_P / 64);
+    const bool hist2 = !want_stats && !dbg && sky && heavy_q > 0;
+    const bool hist1 = !hist2 && !want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * full_waves);
+    (void)waves;
     if (hist1 || hist2) {
-        const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups, (long long)o.textures};
+        const long long key[8] = {P.W, P.H, P.row0, P.row_step, P.n_rows, P.spp, P.n_groups,
+                                  (long long)o.textures | (hist2 ? 2 : 1) << 8};
         int r;
         const int cap0 = s->hist_cap;
         if ((r = ensure_history(s, P.n_groups, key, st)) != RT_OK) return r;
