@@ -91,8 +91,12 @@ int main(int argc, char** argv) {
     }
     if (frames < 1 || spp < 1 || gpus < 1 || ranks < 0 || in_flight < 0 || in_flight > 8) { usage(); return 2; }
     // frames in flight use a stream each: HIP maps streams round-robin onto GPU_MAX_HW_QUEUES
-    // hardware queues (4 by default), and streams sharing a queue serialise
-    if (in_flight > 1) setenv("GPU_MAX_HW_QUEUES", "16", 0);
+    // hardware queues (4 by default), and streams sharing a queue serialise.
+    // The HIP runtime reads it when librt_amd.so's kernels are registered, before main: set it
+    // in the environment (GPU_MAX_HW_QUEUES=16 rtracer ... --in-flight 8).
+    if (in_flight > 1 && !getenv("GPU_MAX_HW_QUEUES"))
+        std::fprintf(stderr, "note: GPU_MAX_HW_QUEUES is not set; with the HIP default of 4 hardware queues "
+                             "frames in flight share queues\n");
 
     // procedural::gpu::generate with optional canvas override; a bad config is reported
     // and exits (the reference asserts)
@@ -131,7 +135,7 @@ int main(int argc, char** argv) {
             rt_render_opts o;
             rt_render_opts_default(&o);
             o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
-            o.rgba = buf[f % D]; o.stream = st[f % D];
+            o.rgba = buf[f % D]; o.stream = st[f % D]; o.sync = 0;   // asynchronous: frames overlap
             rtamd_detail::check(rt_render(handle, &o, nullptr), "rt_render");
             f++;
         };

@@ -160,8 +160,9 @@ def test_cli_frames_in_flight(oracle, tmp_path, extra):
     its own stream (single device, and 8 row-cyclic slices through rt_scene_set_devices with one
     slot's streams per frame); the last frame equals the oracle's."""
     out = str(tmp_path / "p.ppm")
-    r = _run([CLI, "-c", scene_path("world8_stress"), "--width", "240", "--height", "136", "--spp", "2",
-              "--frames", "12", "--out", out] + extra)
+    r = subprocess.run([CLI, "-c", scene_path("world8_stress"), "--width", "240", "--height", "136", "--spp", "2",
+                        "--frames", "12", "--out", out] + extra, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, GPU_MAX_HW_QUEUES="16"))
     assert r.returncode == 0, r.stderr
     assert "ms/frame" in r.stdout
     o = oracle.render(oracle.load(scene_path("world8_stress"), 240, 136), spp=2, nthreads=8, want=("rgba",))

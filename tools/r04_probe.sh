@@ -6,7 +6,7 @@ mkdir -p gpurun_out/r04
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r04/bench0.log 2>&1 || exit 1
 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 150 --timeout-method thread tests/test_gpu_cli.py tests/test_gpu_multi.py tests/test_gpu_fullsize.py tests/test_gpu_pipeline.py -k "cli or multi or config5_full or pipeline or bench_frame" > gpurun_out/r04/pytest_cli_multi.log 2>&1 || exit 1
 for a in "--gpus 1 --ranks 8 --in-flight 8" "--gpus 1 --ranks 8 --in-flight 4" "--gpus 1 --ranks 8 --in-flight 1" "--in-flight 8" "--in-flight 1"; do
-  timeout -k 10 120 ./gpu-ray-tracer_amd/rtracer -c scenes/world8_stress.json --width 1920 --height 1080 --spp 8 --frames 40 $a >> gpurun_out/r04/cli_inflight.log 2>&1 || exit 1
+  GPU_MAX_HW_QUEUES=16 timeout -k 10 120 ./gpu-ray-tracer_amd/rtracer -c scenes/world8_stress.json --width 1920 --height 1080 --spp 8 --frames 40 $a >> gpurun_out/r04/cli_inflight.log 2>&1 || exit 1
 done
 # A/B: heavy-first by work (RT_HEAVY_Q=6) vs off (0)
 bash tools/ab_env.sh r04/ab_heavy RT_HEAVY_Q 0 6 3 > gpurun_out/r04/ab_heavy.log 2>&1 || exit 1
