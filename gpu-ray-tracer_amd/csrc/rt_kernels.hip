@@ -1270,15 +1270,9 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
 // MODE bit 6 (PROF): profiling variant of the fast kernel -- wave-level step counts and
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
-// MODE bit 8 (B768): 768-thread blocks (12 waves, 3 per SIMD: a 168-VGPR budget) for the
-// unparked ordered-tree kernels of scenes whose tree leaves no LDS for parking (world16, config
-// 5): the 128-VGPR form of those kernels spills to scratch (§3.4).
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128,
-              M_B768 = 256;
-__host__ __device__ constexpr int trace_block(int mode) { return (mode & M_B768) ? 768 : TRACE_BLOCK_P; }
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128;
 template <int NS, bool LDS, int MODE>
-__global__ __launch_bounds__(trace_block(MODE)) void trace_kernel(TraceParams P_arg, SceneView S) {
-    static_assert(!((MODE & M_B768) && (MODE & M_PARK)), "the parking area is laid out for TRACE_BLOCK_P lanes");
+__global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     (void)P_arg;                                               // read in place: kparams()
     KTP& P = kparams();
@@ -2693,17 +2687,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
     const bool shade = park && ft && S.tri_ax && !prof &&
                        lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    // B768 (RT_B768=0 in the environment turns it off): the unparked ordered-tree kernels run
-    // 768-thread blocks with a 168-VGPR budget instead of spilling at 128
-    static const bool b768_on = [] { const char* e = getenv("RT_B768"); return !e || atoi(e) != 0; }();
-    const bool b768 = b768_on && ft && !park && ns <= 2;
-    int tb = TRACE_BLOCK_P;                                    // threads per block of the chosen kernel
-    if (tex && ft && b768) {
-        constexpr int TF = M_TEX | M_FT | M_B768, TA = M_TEX | M_FT | M_AXIS | M_B768;
-        fn = ns <= 0 ? (S.tri_ax ? (const void*)trace_kernel<0, true, TA> : (const void*)trace_kernel<0, true, TF>)
-                     : (S.tri_ax ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<2, true, TF>);
-        tb = 768;
-    } else if (tex && ft) {                                    // textured fast frames: ordered LBVH, unparked
+    if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
         constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
         fn = S.tri_ax ? (ns <= 2 ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<NG, true, TA>)
                       : (ns <= 2 ? (const void*)trace_kernel<2, true, TF> : (const void*)trace_kernel<NG, true, TF>);
@@ -2721,10 +2705,6 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         constexpr int PA = M_PARK | M_FT | M_AXIS;
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, PA> : ns <= 2 ? (const void*)trace_kernel<2, true, PA>
                                                                  : (const void*)trace_kernel<NG, true, PA>;
-    } else if (ft && b768) {
-        constexpr int FB = M_FT | M_B768;
-        fn = ns <= 0 ? (const void*)trace_kernel<0, true, FB> : (const void*)trace_kernel<2, true, FB>;
-        tb = 768;
     } else if (ft) {
         constexpr int PF = M_PARK | M_FT;
         fn = park ? (ns <= 0 ? (const void*)trace_kernel<0, true, PF> : ns <= 2 ? (const void*)trace_kernel<2, true, PF>
@@ -2740,7 +2720,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, tb, shm) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
     const int waves_needed = P.n_groups;
     // Frames in flight: a launch issued while the scene's previous frame is still running takes
     // half the CUs.  A persistent block holds its CU (the LDS image) until its slowest wave
@@ -2764,9 +2744,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         }
         if (running) cap = std::max(1, cap / 2);
     }
-    int blocks = std::min(cap, (waves_needed + tb / 64 - 1) / (tb / 64));
+    int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
-    P.heavy_cap = std::max(2 * blocks * (tb / 64), P.n_groups / 4);   // a bound, not a target
+    P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     // longest-first history (fast frames): valid while the launch layout is unchanged
     // Only where a wave runs few groups (1080p 8-way row slices: ~8 per wave): with more (63
     // for a whole 1080p frame, 16 for a 4-way slice) the dynamic queues already balance the
@@ -2774,7 +2754,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // (measured, four frames in flight, ms per frame with / without: whole frame 0.919 / 0.914,
     // 4-way 0.360 / 0.360, 8-way 0.179-0.186 / 0.200-0.204; profiles/r02/hist_policy.log).
     P.hist = 0;
-    const long long waves = (long long)blocks * (tb / 64);
+    const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
     // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
     const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
     // Heavy-first by work (hist = 2) where groups per wave are many: a group whose samples took
@@ -2787,7 +2767,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // skips them in the normal queues; hist = 2 flags by work and lists nothing), so the history
     // key includes the mode and a change of mode resets the flags.
     static const int heavy_q = [] { const char* e = getenv("RT_HEAVY_Q"); return e ? atoi(e) : RT_HEAVY_Q_DEFAULT; }();
-    const long long full_waves = (long long)s->n_cu * per_cu * (tb / 64);
+    const long long full_waves = (long long)s->n_cu * per_cu * (TRACE_BLOCK_P / 64);
     const bool hist2 = !want_stats && !dbg && sky && heavy_q > 0;
     const bool hist1 = !hist2 && !want_stats && !dbg && (prof || (long long)P.n_groups <= RT_HIST_GROUPS_PER_WAVE * full_waves);
     (void)waves;
@@ -2835,7 +2815,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
     }
     void* args[] = {&P, &S};
-    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(tb), args, shm, st, sky ? nullptr : e0, e1, 0));
+    HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));
     HIPCHK(hipGetLastError());
     return RT_OK;
 }
