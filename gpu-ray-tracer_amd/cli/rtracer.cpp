@@ -123,6 +123,7 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> host;
     if (in_flight > 0) {                                   // timing: D frames in flight
         const int D = in_flight;
+        const bool split = gpus > 1 || ranks > 1;
         rtamd_detail::check(rt_scene_set_frame_slots(handle, D), "rt_scene_set_frame_slots");
         std::vector<hipStream_t> st(D);
         std::vector<uint32_t*> buf(D);
@@ -135,11 +136,20 @@ int main(int argc, char** argv) {
             rt_render_opts o;
             rt_render_opts_default(&o);
             o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
-            o.rgba = buf[f % D]; o.stream = st[f % D]; o.sync = 0;   // asynchronous: frames overlap
+            o.rgba = buf[f % D]; o.sync = 0;                  // asynchronous: frames overlap
+            // single device: frame f on stream f % D.  Split frames (use_devices) run on the
+            // library's per-slot streams; a caller stream would only add event waits, which block
+            // whatever else HIP mapped onto that stream's hardware queue
+            o.stream = split ? nullptr : st[f % D];
             rtamd_detail::check(rt_render(handle, &o, nullptr), "rt_render");
             f++;
         };
-        auto wait_all = [&]() { for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]); };
+        auto wait_all = [&]() {
+            if (split) {                                       // every device of the split
+                for (int d = gpus - 1; d >= 0; d--) { (void)hipSetDevice(d); (void)hipDeviceSynchronize(); }
+            }
+            else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
+        };
         for (int k = 0; k < 2 * D; k++) issue();          // warm-up: slots, streams, scheduling history
         wait_all();
         auto from = std::chrono::high_resolution_clock::now();
