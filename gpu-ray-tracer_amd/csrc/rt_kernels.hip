@@ -3327,6 +3327,8 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
         case RT_EXPORT_TRIS:                                   // flattened (mesh) order: hit_tri indexes it
             for (auto& m : h.meshes)
                 for (int i : m.tris) { const auto& t = h.tris[i]; iv.insert(iv.end(), {t.i0, t.i1, t.i2, t.mat}); }
+            // (ABI 3) one record per triangle: the meshes list every triangle exactly once
+            if (iv.size() != 4 * h.tris.size()) return fail(RT_ERR_STATE, "meshes do not cover every triangle once");
             break;
         case RT_EXPORT_MATERIALS:
             for (auto& m : h.mats) {
@@ -3356,6 +3358,7 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
                     const auto& t = h.tris[i];
                     f.insert(f.end(), {(float)t.tex.has, t.tex.tx, t.tex.ty, t.tex.ux, t.tex.uy, t.tex.vx, t.tex.vy});
                 }
+            if (f.size() != 7 * h.tris.size()) return fail(RT_ERR_STATE, "meshes do not cover every triangle once");
             break;
         case RT_EXPORT_ATLAS: {
             const size_t n = h.atlas_rgba.size();

@@ -117,3 +117,15 @@ def test_spp_offsets_match_oracle(rt, oracle):
     for k in range(0, 300, 7):
         assert rt.spp_offset(k) == oracle.spp_offset(k)
     assert rt.spp_offset(0) == (0.0, 0.0)
+
+
+@pytest.mark.parametrize("name", ["world1", "world8", "world8_stress", "world16_tex"])
+def test_triangle_exports_one_record_per_triangle(rt, name):
+    """ABI 3: RT_EXPORT_TRIS / RT_EXPORT_TEXCOORDS list every triangle once, in the flattened
+    mesh order (the index space of hit_tri): as many records as rt_scene_info's n_tris, and each
+    triangle's vertex indices appear exactly once."""
+    s = rt.Scene.load_json(scene_path(name), 32, 24)
+    n = s.info()["n_tris"]
+    tris, tex = s.export("tris"), s.export("texcoords")
+    assert tris.shape == (n, 4) and tex.shape == (n, 7)
+    assert len({tuple(r) for r in tris[:, :3]}) == n or n == 0
