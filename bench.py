@@ -76,6 +76,9 @@ def parse():
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
     p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
+    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "half"), choices=("half", "full", "last-full"),
+                   help="grid of a frame issued while another runs (rt_scene_set_overlap): half the CUs, every CU, "
+                        "or half except the timed region's last frame")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -218,8 +221,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    if overlap and args.grid == "full":
+        scene.set_overlap(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if overlap and args.grid == "last-full" and i == args.steps - 1:
+            scene.set_overlap(True)                         # nothing is issued behind the last frame
         step(not args.no_kernel_timing and not overlap)
     fb.finish()                                             # the last frame's gather + un-permute
     torch.cuda.synchronize()
@@ -227,6 +234,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    if overlap:
+        scene.set_overlap(False)
     tm = scene.timing_collect()
     # latency of one frame issued alone (render + gather + un-permute, waited for); with frames
     # in flight the kernels' event-timed durations come from these lone frames (a launch that
@@ -364,7 +373,8 @@ def main():
                                   if world > 1 else "single GPU",
                    # HIP hardware queues per process (HIP's and the pool's default is 4; bench.py sets 16
                    # so that four render streams + main + collective + copy each get a queue)
-                   "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1},
+                   "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1,
+                   "grid_while_another_runs": args.grid if overlap else "full"},
         "rays_unit": "reference-equivalent rays: every cast_ray of the reference's propagate_ray (SURVEY 8d), "
                      "counted by the counted kernel on the same frame",
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
