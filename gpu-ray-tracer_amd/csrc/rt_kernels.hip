@@ -309,7 +309,8 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 // Per-lane work counters (rays/nodes/leaves/triangle tests, the reference's units) plus
 // wave-level step counts for the profiling experiment (query iterations, child-pair
 // steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
-struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary, live; };
+struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary, live,
+                      cyc_light, cyc_normal, cyc_park; };   // PROF: light step, hit normal + NORMAL-hit step, parking
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
@@ -953,6 +954,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         if ((STATS || PROF) && c_post) { wc.cyc_post += __builtin_amdgcn_s_memtime() - c_post; c_post = 0; }
         // ---- local transitions until this lane waits for a query or is done ----
         while (st == ST_ADVANCE || st == ST_LIGHT) {
+            const unsigned long long cl = PROF ? __builtin_amdgcn_s_memtime() : 0;
             if (st == ST_LIGHT) {
                 if (li < SV().n_lights) {
                     const DLight L = bv.lights[li];
@@ -1000,6 +1002,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     if (fl & 2) { fl &= ~2; pop(); }
                     st = top < 0 ? ST_DONE : ST_ADVANCE;
                 }
+                if (PROF) wc.cyc_light += __builtin_amdgcn_s_memtime() - cl;
                 continue;
             }
             // ST_ADVANCE
@@ -1058,6 +1061,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         float occl = -1.0f;
         if (P.occl_exit && st == ST_WAIT_SHADOW) occl = max_t * (1.0f - 0x1p-21f);
         const float lim = st == ST_WAIT_SHADOW ? max_t : INFINITY;
+        const unsigned long long cpk0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
         if (PARK) {
             float* pk = park;
             int f = 0;
@@ -1071,6 +1075,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             asm volatile("" ::: "memory");
         }
         const unsigned long long c0 = (STATS || PROF) ? __builtin_amdgcn_s_memtime() : 0;
+        if (PROF) wc.cyc_park += c0 - cpk0;
         // (an unlit-skipped shadow step, max_t = -inf, takes no query)
         const bool qa = st == ST_WAIT_NORMAL || (st == ST_WAIT_SHADOW && max_t >= 0.0f);
         const unsigned long long prof_p0 = wc.wpair, prof_l0 = wc.wleaf;
@@ -1097,6 +1102,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                 }
             }
         }
+        const unsigned long long cq1 = PROF ? __builtin_amdgcn_s_memtime() : 0;
         if (PARK) {
             asm volatile("" ::: "memory");
             const float* pk = park;
@@ -1109,6 +1115,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
             fct.x = get(); fct.y = get(); fct.z = get(); fct.w = get();
             if (!OPQ) { rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get(); }
+            if (PROF) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); wc.cyc_park += __builtin_amdgcn_s_memtime() - cq1; }
         }
         unsigned long long c1 = 0;
         if (STATS || PROF) { c1 = __builtin_amdgcn_s_memtime(); wc.cyc_q += c1 - c0; c_post = c1; }
@@ -1117,7 +1124,9 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         V3 hn = v3(0, 0, 0);
         // (opaque scenes: a shadow segment needs neither the normal nor the material -- any hit
         // before the light is opaque, light.cu:44-46)
+        const unsigned long long cn0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
         if (hit && (!OPQ || st == ST_WAIT_NORMAL)) hn = hit_normal(SV(), bv, b, hmat);
+        if (PROF) wc.cyc_normal += __builtin_amdgcn_s_memtime() - cn0;
         if (st == ST_WAIT_NORMAL) {
             if (fl & 1) {
                 fl &= ~1;
@@ -1398,6 +1407,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
         const unsigned long long g_c0 = wc.cyc_q, g_c1 = wc.cyc_leaf, g_c2 = wc.cyc_sample, g_c3 = wc.cyc_post;
+        const unsigned long long g_c4 = wc.cyc_light, g_c5 = wc.cyc_normal, g_c6 = wc.cyc_park;
         const unsigned long long g_m0 = CYC ? __builtin_amdgcn_s_memtime() : 0;
         for (int rd = 0; rd < rounds; rd++) {
             const int k = rd * L + sub_g;
@@ -1511,11 +1521,13 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             if (P.gdur) {
                 P.gdur[g] = (unsigned)dur;
                 if (PROF) {                                    // wave step counts and cycle split of the group
-                    unsigned* c = P.gdur + P.n_groups + 9 * (size_t)g;
+                    unsigned* c = P.gdur + P.n_groups + 12 * (size_t)g;
                     c[0] = (unsigned)(wc.wq - g_q0); c[1] = (unsigned)(wc.wpair - g_p0);
                     c[2] = (unsigned)(wc.wleaf - g_l0); c[3] = (unsigned)(wc.wtri - g_r0);
                     c[4] = (unsigned)(wc.cyc_q - g_c0); c[5] = (unsigned)(wc.cyc_leaf - g_c1);
                     c[6] = (unsigned)(wc.cyc_sample - g_c2); c[7] = (unsigned)(wc.cyc_post - g_c3);
+                    c[9] = (unsigned)(wc.cyc_light - g_c4); c[10] = (unsigned)(wc.cyc_normal - g_c5);
+                    c[11] = (unsigned)(wc.cyc_park - g_c6);
                     c[8] = (unsigned)(__builtin_amdgcn_s_memtime() - g_m0);
                 }
             }
@@ -3753,9 +3765,11 @@ int rt_frame_work(rt_scene* s, const rt_render_opts* o, rt_work* w) {
 // as bench.py's rank row0 of row_step renders them.  `reps` frames, each with the per-frame
 // BVH rebuild; the last one (scheduled from the previous frame's history) is recorded.
 // geo = {n_groups, gw, gh, n_gx}; *ms = the last frame's kernel time.  prof = 1: the recorded
-// frame runs the PROF variant (when the scene has one) and out[n_groups + 9 g ..] holds group
+// frame runs the PROF variant (when the scene has one) and out[n_groups + 12 g ..] holds group
 // g's wave queries, child-pair steps, leaf visits, triangle iterations, then shader cycles in
-// queries, in leaf visits, in trace_sample, after queries (state machine), and in the group.
+// queries, in leaf visits, in trace_sample, after queries (state machine), and in the group; then
+// (slots 9-11) cycles in the light step (ST_LIGHT), in the hit normal of a query's step, and in
+// parking (writes before the query, reads after it; the reads also count in the query's cycles).
 int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, int prof, uint32_t* out, int64_t cap,
                       int* geo, double* ms) {
     CHECK_FINISHED(s);
@@ -3773,7 +3787,7 @@ int rt_profile_groups(rt_scene* s, int spp, int row0, int row_step, int reps, in
     HIPCHK(hipMalloc((void**)&d_rgba, (size_t)s->h.cam.W * rows * sizeof(uint32_t)));
     geo[0] = geo[1] = geo[2] = geo[3] = 0;
     reps = std::max(reps, 2);                                 // frame 0 sizes the buffer and seeds the history
-    const int nw = prof ? 10 : 1;                             // prof: + 9 counters per group (PROF kernel)
+    const int nw = prof ? 13 : 1;                             // prof: + 12 counters per group (PROF kernel)
     if ((r = begin_frame(s, sstream(s), true)) != RT_OK) { (void)hipFree(d_rgba); return r; }
     for (int i = 0; i < reps && r == RT_OK; i++) {
         const bool rec = i == reps - 1;

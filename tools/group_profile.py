@@ -38,7 +38,7 @@ def main():
     os.makedirs(out_dir, exist_ok=True)
     for sl in a.slices.split(","):
         step, row0 = (int(x) for x in sl.split(":"))
-        cap = 10 * a.width * a.height
+        cap = 13 * a.width * a.height
         buf = np.zeros(cap, np.uint32)
         geo = np.zeros(4, np.int32)
         ms = ctypes.c_double()
@@ -46,9 +46,9 @@ def main():
                                          ctypes.byref(ms)))
         ng, gw, gh, ngx = (int(x) for x in geo)
         d = buf[:ng].astype(np.float64) / 1e5                  # ms
-        cnt = buf[ng:10 * ng].reshape(ng, 9) if a.prof else None
+        cnt = buf[ng:13 * ng].reshape(ng, 12) if a.prof else None
         np.save(os.path.join(out_dir, "groups_%s_%d_%d%s.npy" % (a.scene, step, row0, "_prof" if a.prof else "")),
-                buf[:10 * ng] if a.prof else buf[:ng])
+                buf[:13 * ng] if a.prof else buf[:ng])
         order = np.argsort(-d)
         top = []
         for g in order[:a.top]:
@@ -57,7 +57,7 @@ def main():
                         "y": [row0 + gy * gh * step, row0 + (gy * gh + gh - 1) * step]})
             if cnt is not None:
                 top[-1]["queries_pairs_leaves_tris"] = [int(x) for x in cnt[g][:4]]
-                top[-1]["kcyc_query_leaf_sample_post_group"] = [round(int(x) / 1e3, 1) for x in cnt[g][4:]]
+                top[-1]["kcyc_query_leaf_sample_post_group_light_normal_park"] = [round(int(x) / 1e3, 1) for x in cnt[g][4:]]
         print(json.dumps({"scene": a.scene, "row_step": step, "row0": row0, "kernel_ms": round(ms.value, 4),
                           "n_groups": ng, "group": [gw, gh], "sum_ms": round(float(d.sum()), 2),
                           "mean_ms": round(float(d.mean()), 5), "p50": round(float(np.percentile(d, 50)), 5),
@@ -67,6 +67,14 @@ def main():
                           "mean_steps": [round(float(x), 1) for x in cnt[:, :4].mean(0)] if cnt is not None else None,
                           "cycle_split_all_groups": ([round(float(cnt[:, k].sum() / max(1, cnt[:, 8].sum())), 3) for k in (4, 5, 6, 7)]
                                                      if cnt is not None else None),
+                          # live groups: more than one wave query (a sky group's one query misses)
+                          "live_groups": int((cnt[:, 0] > 1).sum()) if cnt is not None else None,
+                          "live_mean_steps": ([round(float(x), 2) for x in cnt[cnt[:, 0] > 1][:, :4].mean(0)]
+                                              if cnt is not None else None),
+                          "live_mean_kcyc_query_leaf_sample_post_group_light_normal_park": (
+                              [round(float(x) / 1e3, 1) for x in cnt[cnt[:, 0] > 1][:, 4:].mean(0)] if cnt is not None else None),
+                          "cycle_split_live_groups": ([round(float(cnt[cnt[:, 0] > 1][:, k].sum() / max(1, cnt[cnt[:, 0] > 1][:, 8].sum())), 3)
+                                                       for k in (4, 5, 6, 7, 9, 10, 11)] if cnt is not None else None),
                           "top": top}), flush=True)
 
 
