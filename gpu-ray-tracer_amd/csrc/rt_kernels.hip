@@ -87,6 +87,12 @@ enum : int {
     PROF_HIST_LEAF = 46,    // [8] their leaf visits
     PROF_END = 54
 };
+// PROF kernels keep the occupancy counters [24, PROF_END) per wave in LDS (a global atomic per wave
+// query on a few shared addresses serialised and perturbed the profile 30x) and add them to d_stats
+// once per wave at the end
+constexpr int PROF_WAVE_SLOTS = 32;
+static_assert(PROF_END - PROF_LANES_PRIMARY <= PROF_WAVE_SLOTS, "per-wave PROF counter slots");
+constexpr size_t PROF_LDS_BYTES = 16 * PROF_WAVE_SLOTS * sizeof(unsigned long long);   // 16 waves per block
 
 enum : int { F_NORMAL = 0, F_REFLECT = 1, F_REFRACT = 2 };
 enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
@@ -310,7 +316,8 @@ struct Best { float time; int inst, tri; float u, v; };     // closest accepted 
 // wave-level step counts for the profiling experiment (query iterations, child-pair
 // steps, leaf visits, triangle-loop iterations -- SIMD work regardless of active lanes).
 struct WaveCounters { unsigned long long rays, nodes, leaves, tris, wq, wpair, wleaf, wtri, cyc_q, cyc_leaf, cyc_all, cyc_sample, cyc_post, wbary, lbary, live,
-                      cyc_light, cyc_normal, cyc_park; };   // PROF: light step, hit normal + NORMAL-hit step, parking
+                      cyc_light, cyc_normal, cyc_park;      // PROF: light step, hit normal, parking
+                      unsigned long long* pc; };            // PROF: this wave's occupancy counters in LDS
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }   // value known wave-uniform
 __device__ __forceinline__ Pose inst_pose(const SceneView& S, const BvhRefs& bv, int ti, int& mesh) {
@@ -1087,18 +1094,18 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             const unsigned long long mu = __ballot(st == ST_WAIT_SHADOW && !qa);
             const int na = __popcll(mn | ms);
             if (lane_id_fresh() == 0) {
-                KTP& Pp = kparams();
-                atomicAdd(&Pp.stats[PROF_LANES_PRIMARY], (unsigned long long)__popcll(mp));
-                atomicAdd(&Pp.stats[PROF_LANES_SECONDARY], (unsigned long long)__popcll(mn & ~mp));
-                atomicAdd(&Pp.stats[PROF_LANES_SHADOW], (unsigned long long)__popcll(ms));
-                atomicAdd(&Pp.stats[PROF_LANES_UNLIT], (unsigned long long)__popcll(mu));
+                unsigned long long* pc = wc.pc - PROF_LANES_PRIMARY;     // index by the d_stats slot
+                pc[PROF_LANES_PRIMARY] += (unsigned long long)__popcll(mp);
+                pc[PROF_LANES_SECONDARY] += (unsigned long long)__popcll(mn & ~mp);
+                pc[PROF_LANES_SHADOW] += (unsigned long long)__popcll(ms);
+                pc[PROF_LANES_UNLIT] += (unsigned long long)__popcll(mu);
                 if (wc.live && na > 0) {
                     const int bk = (na - 1) >> 3;
-                    atomicAdd(&Pp.stats[PROF_LIVE_WQ], 1ull);
-                    atomicAdd(&Pp.stats[PROF_LIVE_LANES], (unsigned long long)na);
-                    atomicAdd(&Pp.stats[PROF_HIST_WQ + bk], 1ull);
-                    atomicAdd(&Pp.stats[PROF_HIST_PAIR + bk], wc.wpair - prof_p0);
-                    atomicAdd(&Pp.stats[PROF_HIST_LEAF + bk], wc.wleaf - prof_l0);
+                    pc[PROF_LIVE_WQ] += 1ull;
+                    pc[PROF_LIVE_LANES] += (unsigned long long)na;
+                    pc[PROF_HIST_WQ + bk] += 1ull;
+                    pc[PROF_HIST_PAIR + bk] += wc.wpair - prof_p0;
+                    pc[PROF_HIST_LEAF + bk] += wc.wleaf - prof_l0;
                 }
             }
         }
@@ -1296,6 +1303,12 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
+    if (PROF) {                                                // this wave's occupancy counters (zeroed)
+        wc.pc = reinterpret_cast<unsigned long long*>(smem + lds_bytes(S, FT, SHADE) +
+                                                       (PARK ? (size_t)park_fields(NS) * 4 * TRACE_BLOCK_P : 0)) +
+                (threadIdx.x >> 6) * PROF_WAVE_SLOTS;
+        if (lane < PROF_WAVE_SLOTS) wc.pc[lane] = 0;
+    }
     // Dynamic group assignment over NQ interleaved queues (queue c owns groups g = c + NQ*j):
     // a wave drains its own queue (c = block % NQ, i.e. one per XCD dispatch slot) then the
     // others.  The next ticket is requested one group ahead so the atomic's latency hides
@@ -1552,6 +1565,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         atomicAdd(&P.stats[17], rt_end - rt_start);             // summed wave lifetimes (same clock)
         atomicMax(&P.stats[18], rt_start);                      // latest start / earliest end
         atomicMin(&P.stats[19], rt_end);
+        if (PROF)
+            for (int i = 0; i < PROF_END - PROF_LANES_PRIMARY; i++)
+                if (wc.pc[i]) atomicAdd(&P.stats[PROF_LANES_PRIMARY + i], wc.pc[i]);
     }
 }
 
@@ -2695,7 +2711,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         {(const void*)trace_kernel<NG, true, 8>, (const void*)trace_kernel<NG, true, 9>,
          (const void*)trace_kernel<NG, true, 10>, (const void*)trace_kernel<NG, true, 11>}};
     const size_t park_bytes = (size_t)park_fields(ns <= 0 ? 0 : 2) * 4 * TRACE_BLOCK_P;
-    const bool park = !tex && mode == 0 && use_lds && lds + park_bytes <= (size_t)PARK_LDS_LIMIT;
+    const bool park = !tex && mode == 0 && use_lds && lds + park_bytes + (prof ? PROF_LDS_BYTES : 0) <= (size_t)PARK_LDS_LIMIT;
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
     const bool shade = park && ft && S.tri_ax && !prof &&
                        lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
@@ -2729,7 +2745,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0);
+    const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0) +
+                       (prof ? PROF_LDS_BYTES : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
