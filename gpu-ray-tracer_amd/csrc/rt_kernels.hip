@@ -100,7 +100,13 @@ enum : int { PH_NORMAL = 1, PH_SHADOW = 2, PH_DONE = 3 };
 __device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b : a; }   // std::max
 // powf of the reference (nvcc pow(float,float)); evaluated in double and rounded:
 // agrees with glibc powf except for 1-ulp cases.
+#if defined(RT_EXP_POW) && RT_EXP_POW == 1
+__device__ __noinline__ float pow_ref(float x, float y) { return x * y; }   // EXPERIMENT (wrong values): pow's cost bound
+#elif defined(RT_EXP_POW) && RT_EXP_POW == 2
+__device__ __noinline__ float pow_ref(float x, float y) { return powf(x, y); }   // EXPERIMENT: single-precision pow
+#else
 __device__ __noinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }   // rare: kept out of line
+#endif
 // pow_ref with the C99 / IEEE special cases that dominate the shading calls answered
 // inline (every powf and pow agree on them bit for bit, F.9.4.4): pow(x, +-0) = 1 (the
 // materials without "alpha"), pow(1, y) = 1, pow(+-0, y > 0) = +0 except -0 for odd integer
