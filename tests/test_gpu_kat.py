@@ -89,6 +89,22 @@ def test_device_pow_within_one_ulp(gpu):
     assert ulp.max() <= 1
 
 
+def test_device_pow_shading_domain(gpu):
+    """pow as the shading uses it (phong.cu:27-32: max(dot, 0) ** alpha, x in [0, 1]; light.cu:18-25
+    and scene.cu:14-22: Kt ** t and t ** Kt): within 1 ulp of the correctly rounded value and of the
+    oracle's glibc powf, on dense grids of x."""
+    x = np.concatenate([np.linspace(0, 1, 200001, dtype=np.float32), np.geomspace(1e-30, 1, 50000).astype(np.float32),
+                        np.linspace(1, 50, 50000, dtype=np.float32)])
+    for yv in (0.6, 0.7, 0.8, 1.5, 2.5, 10.0):
+        y = np.full_like(x, yv)
+        out = gpu.kat_device("pow", x, y)[:, 0]
+        exact = np.power(x.astype(np.float64), y.astype(np.float64)).astype(np.float32)
+        glibc = np.power(x, y)                    # float32 numpy power is libm powf (the oracle's pow)
+        for ref in (exact, glibc):
+            ulp = np.abs(out.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+            assert ulp.max() <= 1, (yv, int(ulp.max()))
+
+
 def test_filtered_triangle_equals_exact(gpu):
     """tri_accept_f (filtered) == Triangle::hit + the t >= 1e-5 acceptance, bit for bit, on the
     edge-dense golden vectors (the reference's own geometry.h produced them)."""
