@@ -364,6 +364,43 @@ RT_HD bool tri_inside_f(V3 a, V3 b, V3 c, float area, float inv_area, const Ray&
 // when |d_ax| < 1e-5 (the reference rejects: every comparison with NaN fails).
 RT_HD float axis_plane_t(float a_ax, float o_ax, float inv_ax) { return inv_ax * (a_ax - o_ax); }
 
+// x^y for float x > 0 and y with |y ln x| <= 700, in double and rounded once to float: the
+// same value as (float)pow((double)x, (double)y) except when x^y lies within ~2^-45 (relative)
+// of a float rounding midpoint, and in every case one of the two floats around x^y, so within
+// 1 ulp of glibc powf (which is within 0.82 ulp).  Returns false outside that domain.
+//   log x = e ln2 + 2 atanh(s), s = (m - 1)/(m + 1), m in [sqrt(1/2), sqrt(2)): m - 1 and m + 1
+//   are exact (m carries x's 24 bits), the division is correctly rounded, |s| <= 0.1716 and the
+//   series to s^19 leaves < 2^-60; e ln2 = e LN2_HI (exact, |e| <= 149) + e LN2_LO.
+//   exp z = 2^k exp r, k = rint(z / ln2), |r| <= 0.3466 + 2^-40: Taylor to r^12 leaves < 2^-52.
+// Rounding: |error of z| <= 2^-52 (|z| + 1), so the relative error of the double is < 2^-44
+// for the float range (|z| < 104) and below 2^-51 on the shading's |z| < 2.
+constexpr double POW_LN2_HI = 6.93147180369123816490e-01;   // 0x3fe62e42fee00000 (32 bits)
+constexpr double POW_LN2_LO = 1.90821492927058770002e-10;   // ln2 - POW_LN2_HI
+RT_HD bool pow_pos(float xf, float yf, float& out) {
+    if (!(xf > 0.0f) || !(fabsf(xf) <= 3.4028235e38f) || !(fabsf(yf) <= 3.4028235e38f)) return false;
+    int e;
+    double m = frexp((double)xf, &e);                   // [0.5, 1)
+    if (m < 0.70710678118654752440) { m = 2.0 * m; e -= 1; }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double p = 2.0 / 19;
+    p = fma(p, s2, 2.0 / 17); p = fma(p, s2, 2.0 / 15); p = fma(p, s2, 2.0 / 13);
+    p = fma(p, s2, 2.0 / 11); p = fma(p, s2, 2.0 / 9);  p = fma(p, s2, 2.0 / 7);
+    p = fma(p, s2, 2.0 / 5);  p = fma(p, s2, 2.0 / 3);
+    const double lm = fma(s * s2, p, 2.0 * s);          // log m
+    const double lx = (double)e * POW_LN2_HI + (lm + (double)e * POW_LN2_LO);
+    const double z = (double)yf * lx;
+    if (!(fabs(z) <= 700.0)) return false;
+    const double k = rint(z * 1.44269504088896340736);
+    const double r = fma(-k, POW_LN2_LO, fma(-k, POW_LN2_HI, z));
+    double q = 1.0 / 479001600;                         // 1/12!
+    q = fma(q, r, 1.0 / 39916800); q = fma(q, r, 1.0 / 3628800); q = fma(q, r, 1.0 / 362880);
+    q = fma(q, r, 1.0 / 40320);    q = fma(q, r, 1.0 / 5040);    q = fma(q, r, 1.0 / 720);
+    q = fma(q, r, 1.0 / 120);      q = fma(q, r, 1.0 / 24);      q = fma(q, r, 1.0 / 6);
+    q = fma(q, r, 0.5);            q = fma(q, r, 1.0);           q = fma(q, r, 1.0);
+    out = (float)ldexp(q, (int)k);
+    return true;
+}
+
 // Host-built record of a triangle for the axis-plane path (rt_kernels.hip, cast_local).
 // code: bits 0-1 axis (3 = general triangle), bit 2 = the next triangle of the mesh has the
 // same axis and plane coordinate (identical t: when no lane accepts this plane crossing, the

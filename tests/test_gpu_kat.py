@@ -103,6 +103,27 @@ def test_device_pow_shading_domain(gpu):
         for ref in (exact, glibc):
             ulp = np.abs(out.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
             assert ulp.max() <= 1, (yv, int(ulp.max()))
+        # pow_pos (rt_math.h) rounds a double within 2^-44 of x^y: the same float as the library's
+        # double pow rounded, bar midpoint cases far rarer than these grids (0 of 4e7 on the host)
+        assert np.array_equal(out.view(np.int32), exact.view(np.int32)), yv
+
+
+def test_device_pow_wide_domain(gpu):
+    """pow over random positive floats and exponents, including the ranges pow_pos hands to the
+    library (|y ln x| > 700, x = 0, inf): equal to (float)pow(double, double), within 1 ulp of powf."""
+    rng = np.random.default_rng(11)
+    bits = rng.integers(0, 0x7f800000, 400000, dtype=np.int64).astype(np.uint32)
+    x = bits.view(np.float32)
+    y = (rng.uniform(-40, 40, x.size) * np.where(np.arange(x.size) % 3 == 0, 1.0, 0.05)).astype(np.float32)
+    x[:4] = [0.0, np.inf, 1.0, 3.0]
+    y[:4] = [0.7, 0.7, 1e30, 1e30]
+    out = gpu.kat_device("pow", x, y)[:, 0]
+    with np.errstate(over="ignore", under="ignore"):
+        exact = np.power(x.astype(np.float64), y.astype(np.float64)).astype(np.float32)
+        glibc = np.power(x, y)
+    assert np.array_equal(out.view(np.int32), exact.view(np.int32))
+    ulp = np.abs(out.view(np.int32).astype(np.int64) - glibc.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1
 
 
 def test_filtered_triangle_equals_exact(gpu):
