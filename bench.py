@@ -76,9 +76,11 @@ def parse():
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
     p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
-    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "half"), choices=("half", "full", "last-full"),
-                   help="grid of a frame issued while another runs (rt_scene_set_overlap): half the CUs, every CU, "
-                        "or half except the timed region's last frame")
+    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "stream"),
+                   choices=("stream", "half", "full", "last-full"),
+                   help="grid of the timed frames (rt_scene_set_overlap): stream = half the CUs for every frame, "
+                        "the first included (RT_OVERLAP_STREAM); half = half the CUs for a frame issued while "
+                        "another runs; full = every CU; last-full = half except the timed region's last frame")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -223,6 +225,8 @@ def main():
     torch.cuda.synchronize()
     if overlap and args.grid == "full":
         scene.set_overlap(True)
+    if overlap and args.grid == "stream":
+        scene.set_overlap(False, stream=True)               # the timed frames are issued back to back
     t0 = time.perf_counter()
     for i in range(args.steps):
         if overlap and args.grid == "last-full" and i == args.steps - 1:
@@ -374,7 +378,7 @@ def main():
                    # HIP hardware queues per process (HIP's and the pool's default is 4; bench.py sets 16
                    # so that four render streams + main + collective + copy each get a queue)
                    "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1,
-                   "grid_while_another_runs": args.grid if overlap else "full"},
+                   "grid_timed_frames": args.grid if overlap else "full"},
         "rays_unit": "reference-equivalent rays: every cast_ray of the reference's propagate_ray (SURVEY 8d), "
                      "counted by the counted kernel on the same frame",
         "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),

@@ -2779,8 +2779,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // optional second half of the grid gated on later frames being queued
     // (profiles/r03/ab_grid/readback.log): such callers set RT_OVERLAP_FULL.
     int cap = s->n_cu * per_cu;
-    if (s->n_slots >= 4 && s->overlap == RT_OVERLAP_HALF) {
-        bool running = false;                                  // another frame of the scene in flight
+    if (s->n_slots >= 4 && s->overlap != RT_OVERLAP_FULL) {
+        bool running = s->overlap == RT_OVERLAP_STREAM;        // another frame of the scene in flight, or a stream
         for (int i = 1; i < s->n_slots && !running; i++) {
             const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
             running = s->slot_pending[sl] && hipEventQuery(s->slot_done[sl]) == hipErrorNotReady;
@@ -3594,7 +3594,8 @@ int rt_scene_set_frame_slots(rt_scene* s, int n) {
 
 int rt_scene_set_overlap(rt_scene* s, int policy) {
     CHECK_SCENE(s);
-    if (policy != RT_OVERLAP_HALF && policy != RT_OVERLAP_FULL) return fail(RT_ERR_ARG, "overlap policy: RT_OVERLAP_HALF or RT_OVERLAP_FULL");
+    if (policy != RT_OVERLAP_HALF && policy != RT_OVERLAP_FULL && policy != RT_OVERLAP_STREAM)
+        return fail(RT_ERR_ARG, "overlap policy: RT_OVERLAP_HALF, RT_OVERLAP_FULL or RT_OVERLAP_STREAM");
     s->overlap = policy;
     return RT_OK;
 }

@@ -405,11 +405,12 @@ class Scene:
         overlap (rt_scene_set_frame_slots)."""
         _check(lib().rt_scene_set_frame_slots(self._h, int(n)))
 
-    def set_overlap(self, full):
+    def set_overlap(self, full, stream=False):
         """Grid of a frame issued while another frame of the scene runs (four or more slots): False =
         half the CUs (default; device-resident pipelines), True = every CU (pipelines that
-        copy each frame to the host) (rt_scene_set_overlap)."""
-        _check(lib().rt_scene_set_overlap(self._h, 1 if full else 0))
+        copy each frame to the host); stream=True: half the CUs for every frame, the first
+        included, while frames are issued back to back (rt_scene_set_overlap)."""
+        _check(lib().rt_scene_set_overlap(self._h, 2 if stream else 1 if full else 0))
 
     def timing_collect(self):
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()

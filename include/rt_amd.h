@@ -187,8 +187,12 @@ int rt_scene_set_frame_slots(rt_scene* s, int n_slots);
  * share the GPU and a block's tail (its slowest wave) holds fewer CUs; RT_OVERLAP_FULL =
  * every CU, as a frame issued alone gets.  HALF measured faster for device-resident
  * pipelines (frame -3%, row slices -4..-11%), FULL for pipelines that copy every frame to the
- * host (-12%).  Images are identical either way.  Host-side state. */
-enum { RT_OVERLAP_HALF = 0, RT_OVERLAP_FULL = 1 };
+ * host (-12%).  RT_OVERLAP_STREAM = half the CUs for every frame, the
+ * first of a stream included, for callers that issue frames back to back: the first two
+ * frames then run side by side instead of the second waiting for the first's tail (20-frame
+ * streams -2%), but a frame issued alone takes half the GPU, so set it for the stream only.
+ * Images are identical either way.  Host-side state. */
+enum { RT_OVERLAP_HALF = 0, RT_OVERLAP_FULL = 1, RT_OVERLAP_STREAM = 2 };
 int rt_scene_set_overlap(rt_scene* s, int policy);
 
 /* Multi-GPU frames from one host process (the reference's single-device

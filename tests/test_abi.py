@@ -82,10 +82,12 @@ def test_frame_slots_arguments(rt):
 
 
 def test_overlap_policy_arguments(rt):
-    """rt_scene_set_overlap takes RT_OVERLAP_HALF (0) or RT_OVERLAP_FULL (1) (host-side state)."""
+    """rt_scene_set_overlap takes RT_OVERLAP_HALF (0), RT_OVERLAP_FULL (1) or RT_OVERLAP_STREAM (2)
+    (host-side state)."""
     s = rt.Scene.load_json(scene_path("world1"), 16, 16)
     s.set_frame_slots(4)
     s.set_overlap(True)
+    s.set_overlap(False, stream=True)
     s.set_overlap(False)
-    for bad in (2, -1):
+    for bad in (3, -1):
         assert rt.lib().rt_scene_set_overlap(s._h, bad) == rt.RT_ERR_ARG

@@ -44,6 +44,26 @@ def test_frame_slots_streams_identical(gpu, scene, spp, depth):
     assert all(torch.equal(p, ref) for p in pipe.parts)
 
 
+@pytest.mark.parametrize("policy", ["half", "full", "stream"])
+def test_overlap_policies_identical(gpu, policy):
+    """rt_scene_set_overlap (RT_OVERLAP_HALF / FULL / STREAM; four or more slots, so frames take
+    half or all of the CUs) changes only the grids: the frames are the serial frame."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+    import rtamd.dist as rtdist
+    w, h, spp, depth = 320, 180, 8, 8
+    ref = _serial(gpu, "world8_stress", w, h, spp)
+    s = gpu.Scene.load_json(scene_path("world8_stress"), w, h)
+    s.set_frame_slots(depth)
+    s.set_overlap(policy == "full", stream=policy == "stream")
+    pipe = rtdist.FramePipeline(w, h, 1, 0, "cuda", depth=depth)
+    for k in range(12):
+        pipe.step(k, lambda buf, st: s.render_device(spp=spp, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream))
+    torch.cuda.synchronize()
+    assert torch.equal(pipe.finish(), ref)
+    assert all(torch.equal(p, ref) for p in pipe.parts)
+
+
 class _Work:
     """Like a torch.distributed Work: wait() makes the current stream wait for the copies
     issued on the stream current at the gather."""

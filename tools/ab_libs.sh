@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 for i in $(seq 1 "$ROUNDS"); do
   for lib in "$@"; do
     n=$(basename "$lib" .so)
-    RTAMD_LIB=$lib timeout -k 10 240 python3 -u "$R/bench.py" --steps 60 --warmup 5 --no-cpu-baseline \
+    RTAMD_LIB=$lib timeout -k 10 240 python3 -u "$R/bench.py" --steps ${STEPS:-60} --warmup 5 --no-cpu-baseline \
       > "$OUT/bench_${n}_$i.log" 2>&1 || { echo "bench $n round $i failed"; exit 1; }
     python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%-12s round %s frame_ms %.4f trace %.4f latency %.4f readback %.4f' % (sys.argv[2], sys.argv[3], d['frame_ms'], d['trace_kernel_ms'], d['frame_latency_ms'], d['ms_per_step_with_readback']))" "$OUT/bench_${n}_$i.log" "$n" $i
     if [ "$SLICES" = 1 ]; then
