@@ -221,6 +221,9 @@ struct BvhRefs {
 #ifndef RT_HIST_GROUPS_PER_WAVE
 #define RT_HIST_GROUPS_PER_WAVE 12  // longest-first history only at <= this many groups per wave
 #endif
+#ifndef RT_SMALL_FRAME_GPW
+#define RT_SMALL_FRAME_GPW 48       // groups per wave (half grid) below which overlapping frames take a quarter of the CUs
+#endif
 #ifndef RT_HEAVY_Q_DEFAULT
 #define RT_HEAVY_Q_DEFAULT 6        // hist = 2: a group of >= this many wave queries is heavy
 #endif
@@ -2785,7 +2788,14 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
             const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
             running = s->slot_pending[sl] && hipEventQuery(s->slot_done[sl]) == hipErrorNotReady;
         }
-        if (running) cap = std::max(1, cap / 2);
+        // Small frames (row slices of N >= 4 ranks: under ~48 groups per wave on half the CUs)
+        // take a quarter: four frames' blocks share the GPU, each block runs twice the groups,
+        // so its LDS staging and its slowest wave's tail weigh half as much.  Measured per-rank
+        // ms per frame, 60-frame streams, same box (profiles/r04/grid_div.log): N = 8 0.112 ->
+        // 0.101, N = 4 0.175 -> 0.171; whole frames unchanged by it (0.597 / 0.599), kept at half.
+        const long long half_waves = (long long)(cap / 2) * (TRACE_BLOCK_P / 64);
+        const int div = (long long)P.n_groups < RT_SMALL_FRAME_GPW * half_waves ? 4 : 2;
+        if (running) cap = std::max(1, cap / div);
     }
     int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
