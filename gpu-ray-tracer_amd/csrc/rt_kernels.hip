@@ -102,19 +102,11 @@ __device__ __forceinline__ float max_std(float a, float b) { return (a < b) ? b 
 // agrees with glibc powf except for 1-ulp cases.  pow_pos (rt_math.h)
 // answers x > 0 with |y ln x| <= 700 in about 40 double operations; the rest (x <= 0, inf,
 // nan, overflow and underflow far outside float range) take the library's double pow.
-#if defined(RT_EXP_POW) && RT_EXP_POW == 1
-__device__ __noinline__ float pow_ref(float x, float y) { return x * y; }   // EXPERIMENT (wrong values): pow's cost bound
-#elif defined(RT_EXP_POW) && RT_EXP_POW == 2
-__device__ __noinline__ float pow_ref(float x, float y) { return powf(x, y); }   // EXPERIMENT: single-precision pow
-#elif defined(RT_EXP_POW) && RT_EXP_POW == 3
-__device__ __noinline__ float pow_ref(float x, float y) { return (float)pow((double)x, (double)y); }   // EXPERIMENT: round 3's form
-#else
 __device__ __forceinline__ float pow_lib(float x, float y) { return (float)pow((double)x, (double)y); }
 __device__ __noinline__ float pow_ref(float x, float y) {   // rare: kept out of line
     float o;
     return pow_pos(x, y, o) ? o : pow_lib(x, y);
 }
-#endif
 // pow_ref with the C99 / IEEE special cases that dominate the shading calls answered
 // inline (every powf and pow agree on them bit for bit, F.9.4.4): pow(x, +-0) = 1 (the
 // materials without "alpha"), pow(1, y) = 1, pow(+-0, y > 0) = +0 except -0 for odd integer
