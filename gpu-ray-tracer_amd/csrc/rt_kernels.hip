@@ -2104,6 +2104,7 @@ struct rt_scene {
 #define RT_OVERLAP_DEFAULT RT_OVERLAP_HALF   // (RT_OVERLAP_FULL: the A/B arm of round 3's policy)
 #endif
     int overlap = RT_OVERLAP_DEFAULT;                                // rt_scene_set_overlap
+    int ranks_per_device = 1;                    // > 1: virtual ranks of rt_scene_set_devices share this device
     unsigned slot_inst_gen = 0;                  // instance generation the current slot's arrays hold
     unsigned inst_gen = 1;                       // generation of the host instance array (set_trans bumps it)
     unsigned shape_gen = 0;                      // generation n_real / fdepth were computed for
@@ -2786,7 +2787,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         // ms per frame, 60-frame streams, same box (profiles/r04/grid_div.log): N = 8 0.112 ->
         // 0.101, N = 4 0.175 -> 0.171; whole frames unchanged by it (0.597 / 0.599), kept at half.
         const long long half_waves = (long long)(cap / 2) * (TRACE_BLOCK_P / 64);
-        const int div = (long long)P.n_groups < RT_SMALL_FRAME_GPW * half_waves ? 4 : 2;
+        // (Not with virtual ranks, several slices of one frame per device from one scene: those
+        // slices share frame slots, and a quarter measured slower there: --gpus 1 --ranks 8 per
+        // slice 0.153 -> 0.173 ms, profiles/r04/grid_div.log.)
+        const int div = ((long long)P.n_groups < RT_SMALL_FRAME_GPW * half_waves && s->ranks_per_device == 1) ? 4 : 2;
         if (running) cap = std::max(1, cap / div);
     }
     int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
@@ -3020,6 +3024,7 @@ void free_multi(rt_scene* s) {
     MultiDev* m = s->multi;
     if (!m) return;
     s->multi = nullptr;
+    s->ranks_per_device = 1;
     free_multi_slots(m);
     Rccl* R = rccl(nullptr);
     for (size_t i = 0; i < m->comms.size(); i++) {
@@ -3069,6 +3074,7 @@ int setup_multi(rt_scene* s, MultiDev* m, Rccl* R) {
         rp->h = s->h; rp->finished = true;
         rp->h.atlas_rgba.clear();
         rp->overlap = s->overlap;
+        rp->ranks_per_device = m->per_dev;
         m->reps.push_back(rp);
         m->inst_gen.push_back(0);
         const int saved = g_device;
@@ -3634,6 +3640,7 @@ int rt_scene_set_devices(rt_scene* s, const int* devices, int n_devices, int n_r
     m->reps.push_back(s);
     m->inst_gen.push_back(s->inst_gen);
     s->multi = m;
+    s->ranks_per_device = m->per_dev;
     return RT_OK;
 }
 
