@@ -737,16 +737,17 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
 // diffuse + specular: phong's factor of the incoming light
 // tl_len = len(to_light), tl_neg_unit = normalized(neg(to_light)) (the shadow ray's direction
 // negated: the light step has them)
-__device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 ray_dir, V3 to_light, float tl_len,
-                                           V3 tl_neg_unit) {
+__device__ __forceinline__ V4 phong_factor(const DMat& m, V4 kd, V3 nrm, V3 nrm_unit, V3 ray_dir, V3 to_light,
+                                           float tl_len, V3 tl_neg_unit) {
     float nd = max_std(dot(to_light, nrm), 0.0f);
     V4 diffuse = nd * kd;
-    V3 reflected = reflect_pre(tl_len, tl_neg_unit, normalized(nrm));   // reflect(neg(to_light), nrm)
+    V3 reflected = reflect_pre(tl_len, tl_neg_unit, nrm_unit);         // reflect(neg(to_light), nrm)
     float rd = dot(neg(reflected), ray_dir);
     V4 specular = pow_fast(max_std(rd, 0.0f), m.alpha) * m.Ks;
     return diffuse + specular;
 }
-// phong(m, kd, nrm, incoming, ...) = phong_factor(m, kd, nrm, ...) * incoming (trace_sample's light step)
+// phong(m, kd, nrm, incoming, ...) = phong_factor(m, kd, nrm, normalized(nrm), ...) * incoming (trace_sample's
+// light step)
 
 // RayFrame (scene.cu:81-90).  The top frame's hit point and normal are not kept in
 // registers: while the frame is being lit they equal at(ray, is_time) and is_norm
@@ -931,12 +932,16 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // the same operations in the same order as the reference's phong.  NS = 0 kernels run only scenes without a
 // refractive material (launch_trace): there a shadow ray's light is never attenuated (rv = the
 // light's colour, reloaded after the query), so they park 4 fields fewer.
-constexpr int PARK_FIELDS = 26;
-__host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 22 : PARK_FIELDS; }
+// Parked kernels also park normalized(hit normal), formed once per hit for phong's reflect
+// (every light) and the reflection ray, instead of once per use (same value: frame -1.8%,
+// profiles/r04/ab_nn.log).
+constexpr int PARK_FIELDS = 29;
+__host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 25 : PARK_FIELDS; }
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, int out_p, WaveCounters& wc, float* park, int& nq) {
     constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
+    constexpr bool NN = PARK;                                   // is_nn parked across the queries
     KTP& P0 = kparams();
     Frame cur;
     SavedFrame stk[NS > 0 ? NS : 1];
@@ -947,6 +952,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
     V4 acc = v4(0, 0, 0, 0);
     float is_time = INFINITY;                                   // the sample's shared Isect
     V3 is_norm = v3(0, 0, 0);
+    V3 is_nn = v3(0, 0, 0);                                     // normalized(is_norm) (parked kernels)
     int is_mat = 0;
     V4 is_kd = v4(0, 0, 0, 0);                                  // textured mode: the hit's diffuse colour
     int li = 0;
@@ -1007,7 +1013,8 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     // marks it): no hit, so the light's term is phong's with the unshadowed
                     // light, the same signed zeros.
                     const DMat& mm = bv.mats[is_mat];
-                    fct = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, cur.ray.d, dtl, tl, tn);
+                    fct = phong_factor(mm, TEX ? is_kd : mm.Kd, is_norm, NN ? is_nn : normalized(is_norm), cur.ray.d,
+                                       dtl, tl, tn);
                     if (P.unlit_skip && fct.x == 0.0f && fct.y == 0.0f && fct.z == 0.0f && fct.w == 0.0f)
                         max_t = -INFINITY;
                     q = make_ray(at(to, THRESH), to.d);
@@ -1048,7 +1055,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                     cur.type = F_NORMAL;                           // the child: last_mat, in_obj inherited
                     cur.atten = cur.atten * m.Kr;
                     cur.depth = cur.depth - 1;
-                    cur.ray = make_ray(hp, reflect(cur.ray.d, normalized(is_norm)));
+                    cur.ray = make_ray(hp, reflect(cur.ray.d, NN ? is_nn : normalized(is_norm)));
                 }
             } else if (!OPQ && m.refractive) {                    // F_REFRACT (scene.cu:149-184)
                 dbg(P, me, 3);
@@ -1087,6 +1094,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             put(acc.x); put(acc.y); put(acc.z); put(acc.w);
             put(summed.x); put(summed.y); put(summed.z); put(summed.w);
             put(fct.x); put(fct.y); put(fct.z); put(fct.w);
+            if (NN) { put(is_nn.x); put(is_nn.y); put(is_nn.z); }
             if (!OPQ) { put(rv.x); put(rv.y); put(rv.z); put(rv.w); }
             asm volatile("" ::: "memory");
         }
@@ -1130,6 +1138,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             acc.x = get(); acc.y = get(); acc.z = get(); acc.w = get();
             summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
             fct.x = get(); fct.y = get(); fct.z = get(); fct.w = get();
+            if (NN) { is_nn.x = get(); is_nn.y = get(); is_nn.z = get(); }
             if (!OPQ) { rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get(); }
             if (PROF) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); wc.cyc_park += __builtin_amdgcn_s_memtime() - cq1; }
         }
@@ -1160,6 +1169,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
                 continue;
             }
             is_time = b.time; is_norm = hn; is_mat = hmat;
+            if (NN) is_nn = normalized(hn);
             if (TEX) is_kd = hit_kd(P, bv, b, hmat);
             fl &= ~4;                                              // hit point / normal = at(ray, is_time), is_norm
             if (cur.depth > 0) {                                   // scene.cu:109-121
