@@ -3615,6 +3615,8 @@ int rt_scene_set_overlap(rt_scene* s, int policy) {
     if (policy != RT_OVERLAP_HALF && policy != RT_OVERLAP_FULL && policy != RT_OVERLAP_STREAM)
         return fail(RT_ERR_ARG, "overlap policy: RT_OVERLAP_HALF, RT_OVERLAP_FULL or RT_OVERLAP_STREAM");
     s->overlap = policy;
+    if (s->multi)                                              // the replicas of rt_scene_set_devices too
+        for (rt_scene* rp : s->multi->reps) rp->overlap = policy;
     return RT_OK;
 }
 
