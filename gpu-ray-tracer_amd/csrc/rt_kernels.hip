@@ -219,6 +219,9 @@ struct BvhRefs {
 #ifndef RT_HEAVY_Q_DEFAULT
 #define RT_HEAVY_Q_DEFAULT 6        // hist = 2: a group of >= this many wave queries is heavy
 #endif
+#ifndef RT_HEAVY_STATIC
+#define RT_HEAVY_STATIC 1    // frames issued alone: heavy-list tickets assigned statically (trace_kernel)
+#endif
 #ifndef RT_TPC
 #define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop) over all
                              // groups; 3 vs 2: -0.8% world8_stress, -1.3% world8 (profiles/r01/ab_tpc_v33.log)
@@ -804,6 +807,8 @@ struct TraceParams {
     // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
     const int* live; int live_cap;
     int tpc;                  // work indices per ticket (normal queues)
+    int grid_waves;           // waves of this launch (the heavy list's static rounds)
+    int heavy_static;         // 1: heavy-list tickets assigned statically (frames issued alone)
     int unlit_skip;           // fast frames: no shadow segments for a light whose phong factor is zero (1),
                               // and no phong term for it either (2)
 };
@@ -1356,6 +1361,15 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     // loop without tracing).
     int pend = 0, inflight = 0;
     auto step_of = [&](int q) { return q < 0 ? 1 : kparams().tpc; };
+#if RT_HEAVY_STATIC
+    // A frame issued alone (heavy_static: every block starts at once) deals the heavy list out
+    // statically, wave w taking tickets w, w + W, w + 2W, ... with no atomic: otherwise the
+    // grid's 4096 waves all queue on the one heavy counter before their first group (~100 M
+    // atomics/s: ~40 us).  Lone trace 0.768 -> 0.702 ms (profiles/r04/ab_hs2.log).  Frames that
+    // overlap others keep the counter: their blocks start as CUs free up, and a late block's
+    // static share became the tail (pipelined frame +1.9% with it; profiles/r04/ab_hs.log).
+    int hnext = (int)blockIdx.x * (TRACE_BLOCK_P / 64) + (int)(threadIdx.x >> 6);   // this wave's next heavy ticket
+#endif
     // live lists: tickets [0, 2^k) of a list of n <= 2^k groups visit (t * odd) mod 2^k, a
     // bijection that spreads consecutive tickets over the list (arrival order is roughly
     // raster order, where expensive regions cluster); indices >= n are skipped
@@ -1370,6 +1384,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         unsigned long long a = (unsigned long long)(q < 0 ? &Pq.work[16 * NQ] : &Pq.work[16 * ((q0 + q) % NQ)]);
         asm volatile("" : "+v"(a));
         typedef __attribute__((address_space(1))) int gint;   // keep the global (not flat) atomic
+#if RT_HEAVY_STATIC
+        if (q < 0 && kparams().heavy_static) { pend = hnext; hnext += kparams().grid_waves; inflight = 1; return; }
+#endif
         if (lane == 0) pend = __hip_atomic_fetch_add((gint*)a, step_of(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         inflight = 1;
     };
@@ -2805,6 +2822,8 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     }
     int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
+    P.grid_waves = blocks * (TRACE_BLOCK_P / 64);              // the launch below: dim3(blocks)
+    P.heavy_static = blocks == s->n_cu * per_cu ? 1 : 0;       // every block starts at once (no frame running)
     P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     // longest-first history (fast frames): valid while the launch layout is unchanged
     // Only where a wave runs few groups (1080p 8-way row slices: ~8 per wave): with more (63
