@@ -72,6 +72,13 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-rows", type=int, default=1, help="CPU baseline renders rows y %% k == 0")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--pmc-step", default=os.path.join(ROOT, "profiles", "pmc_step.json"),
+                   help="counters summed over the timed window of this command under rocprofv3 (tools/pmc_step.py)")
+    p.add_argument("--dump-frame", default="",
+                   help="rank 0 saves the last timed frame (gathered, un-permuted RGBA8) as .npy (tests)")
+    p.add_argument("--cpu-runs", type=int, default=3, help="CPU baseline: timed 1-thread frames (median), after one warm-up")
+    p.add_argument("--no-camera-path", action="store_true",
+                   help="skip the moving-camera figure (camera_path: main.cc's key and mouse steps every frame)")
     p.add_argument("--no-kernel-timing", action="store_true",
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
@@ -116,9 +123,15 @@ def cpu_baseline(args, scene_path):
     s = orc.load(scene_path, args.width, args.height)
     k = max(1, args.cpu_sample_rows)
     bvh = 0 if args.brute else 1
-    t = time.perf_counter()
-    fr = orc.render(s, semantics=1, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=1, want=())
-    dt = time.perf_counter() - t
+    # BASELINE.md §3's protocol: one warm-up, then the median of `cpu_runs` timed 1-thread runs
+    # (the warm-up renders every 8th row of the sample: it pages the scene and code in)
+    orc.render(s, semantics=1, use_bvh=bvh, spp=1, row0=0, row_step=8 * k, nthreads=1, want=())
+    runs = []
+    for _ in range(max(1, args.cpu_runs)):
+        t = time.perf_counter()
+        fr = orc.render(s, semantics=1, use_bvh=bvh, spp=1, row0=0, row_step=k, nthreads=1, want=())
+        runs.append(time.perf_counter() - t)
+    dt = sorted(runs)[len(runs) // 2]
     rays = int(fr["stats"][0])
     rows = len(range(0, args.height, k))
     # every core this job may run on (its CPU affinity), not the machine's count: a GPU box shares
@@ -144,8 +157,11 @@ def cpu_baseline(args, scene_path):
     return {
         "value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
         "sample": "%s %dx%d rows y%%%d==0 (%d rows), spp=1, CPU-path semantics of src/raytracer.cc "
-                  "(oracle restatement), 1 thread; %.1f s, %d rays; extrapolated frame at %d spp: %.0f ms"
-                  % (args.scene, args.width, args.height, k, rows, dt, rays, args.spp, dt * k * args.spp * 1e3),
+                  "(oracle restatement), 1 thread; median of %d runs after a warm-up: %.1f s, %d rays; "
+                  "extrapolated frame at %d spp: %.0f ms"
+                  % (args.scene, args.width, args.height, k, rows, len(runs), dt, rays, args.spp, dt * k * args.spp * 1e3),
+        "runs_s": [round(x, 3) for x in runs],
+        "spread": round((max(runs) - min(runs)) / dt, 4),
         "cpu_path_all_cores": {"value": int(fc["stats"][0]) / dc / 1e6, "unit": "Mrays/s", "cores": nthr,
                                "seconds": round(dc, 2), "kind": "port"},
         "gpu_semantics_all_cores": {"value": int(fg["stats"][0]) / dg / 1e6, "unit": "Mrays/s", "cores": nthr,
@@ -153,6 +169,49 @@ def cpu_baseline(args, scene_path):
         "cpu_model": cpu_model, "nproc": os.cpu_count(), "affinity_cores": affinity, "cgroup_cpu_quota": quota,
         "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
     }
+
+
+# main.cc's camera steps (main.cc:19-20, 144-177): the W key translates the camera by
+# (0, 0, MOVE_SPEED) in its own frame; a mouse motion of (xrel, yrel) = (1, 0) turns it by
+# Quat(up, ROT_SPEED * 1) * Quat(right, ROT_SPEED * 0) (rel_mot normalized: (1, 0)).
+MOVE_SPEED, ROT_SPEED = 0.2, 0.01
+
+
+def _quat_axis_angle(axis, theta):
+    """geometry.h:36-41 as a g++ TU computes it: double cos / sin of the float 0.5f * theta,
+    rounded to float (include/rtracer_amd.hpp, tests/test_shim_math.py)."""
+    import math
+    import numpy as np
+    h = float(np.float32(0.5) * np.float32(theta))
+    hc, hs = np.float32(math.cos(h)), np.float32(math.sin(h))
+    a = np.asarray(axis, np.float32)
+    return np.array([a[0] * hs, a[1] * hs, a[2] * hs, hc], np.float32)
+
+
+def _quat_mul(a, b):
+    """geometry.h:161-174 (Hamilton product, the reference's operand order) in float32."""
+    import numpy as np
+    i, j, k, r = [np.float32(x) for x in a]
+    bi, bj, bk, br = [np.float32(x) for x in b]
+    return np.array([i * br + r * bi + j * bk - k * bj, j * br + r * bj + k * bi - i * bk,
+                     k * br + r * bk + i * bj - j * bi, r * br - i * bi - j * bj - k * bk], np.float32)
+
+
+def _normalized(v):
+    """Vec::normalized (linear.h:159-167): (1 / len) * v above the 1e-5 threshold."""
+    import numpy as np
+    v = np.asarray(v, np.float32)
+    n = np.float32(np.sqrt(np.float32(v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]))
+    return (np.float32(1.0) / n) * v if n > np.float32(1e-5) else np.zeros(3, np.float32)
+
+
+def camera_move(scene):
+    """One frame of main.cc's interactive caller: the W key, then a one-pixel mouse motion."""
+    scene.translate_camera((0.0, 0.0, MOVE_SPEED))                         # main.cc:146-148
+    r, u, _ = scene.camera_axes()
+    rot = _quat_mul(_quat_axis_angle(_normalized(u), ROT_SPEED * 1.0),     # main.cc:173-177
+                    _quat_axis_angle(_normalized(r), ROT_SPEED * 0.0))
+    scene.rotate_camera(rot)
 
 
 def main():
@@ -227,6 +286,8 @@ def main():
         scene.set_overlap(True)
     if overlap and args.grid == "stream":
         scene.set_overlap(False, stream=True)               # the timed frames are issued back to back
+    rtamd.profile_marker(1, stream.cuda_stream)             # the timed window starts (tools/pmc_step.py)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if overlap and args.grid == "last-full" and i == args.steps - 1:
@@ -238,6 +299,10 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    rtamd.profile_marker(2, stream.cuda_stream)             # ... and ends
+    if args.dump_frame and rank == 0:
+        import numpy as np
+        np.save(args.dump_frame, fb.frame.cpu().numpy().view(np.uint32))
     if overlap:
         scene.set_overlap(False)
     tm = scene.timing_collect()
@@ -257,6 +322,41 @@ def main():
     lat_ms = sorted(lat)[len(lat) // 2] * 1e3
     if overlap:
         tm = scene.timing_collect()
+    # Moving camera (the reference's real caller moves it every frame, main.cc:140-180): the
+    # same K timed frames with main.cc's key and mouse steps applied before each, so the
+    # previous frame's heavy-group flags (history-driven scheduling) are one pose stale.
+    # Rays in the reference's units from a counted replay of the same poses (untimed).
+    cam_path = None
+    if not args.no_camera_path:
+        pos0, quat0 = scene.camera()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if overlap and args.grid == "full":
+            scene.set_overlap(True)
+        if overlap and args.grid == "stream":
+            scene.set_overlap(False, stream=True)
+        tc0 = time.perf_counter()
+        for i in range(args.steps):
+            camera_move(scene)
+            step(False)
+        fb.finish()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        cam_s = time.perf_counter() - tc0
+        if overlap:
+            scene.set_overlap(False)
+        scene.set_camera(pos0, quat0)
+        cam_rays = 0
+        for i in range(args.steps):
+            camera_move(scene)
+            cst = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
+                                      compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, sync=True,
+                                      stats=True, textures=args.textures)
+            cam_rays += int(cst["rays"])
+        scene.set_camera(pos0, quat0)
+        cam_path = (cam_s, cam_rays)
     # host-readable frames (the reference's post-condition, raytracer.cu:102-120): the same
     # pipeline with an asynchronous copy of every finished frame into pinned host memory;
     # the timed region ends when the last frame is on the host (serial frames: a blocking
@@ -316,6 +416,13 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     rays, nodes, leaves, tris, queries, leaf_lanes = [float(x) for x in local_rays.cpu()]
     elapsed = float(tmax.item())
+    if cam_path:
+        cp = torch.tensor([cam_path[0], float(cam_path[1])], dtype=torch.float64, device=red_dev)
+        cps = cp[1:].clone()
+        if dist:
+            dist.all_reduce(cp[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(cps, op=dist.ReduceOp.SUM)
+        cam_path = (float(cp[0].item()), float(cps[0].item()))
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -416,6 +523,46 @@ def main():
                               "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4),
                               "valu_insts_per_launch": int(issue["SQ_INSTS_VALU"]),
                               "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU)"}
+    # The timed step itself: counters summed over every dispatch between
+    # this command's profile markers under rocprofv3 (tools/profile_step.sh, tools/pmc_step.py;
+    # profiles/pmc_step.json), per step, over this run's ms_per_step.  The lone-launch figures
+    # above describe one frame alone; these describe the pipelined step the metric times.
+    pst = None
+    if os.path.exists(args.pmc_step):
+        try:
+            pst = json.load(open(args.pmc_step)).get("%s_%dx%d_spp%d_n%d" % (args.scene, W, H, args.spp, world))
+        except Exception:
+            pst = None
+    if pst and pst.get("hbm_bytes_per_step"):
+        b = pst["hbm_bytes_per_step"]
+        a = b / (ms_per_step * 1e-3) / 1e9
+        roof["per_step"] = {"traffic": int(b), "achieved": round(a, 2), "frac": round(a / HBM_PEAK_GBS, 5),
+                            "traffic_over_algorithmic": round(b / max(1, algo_bytes), 2),
+                            "gpu_busy_ms_per_step": round(pst.get("gpu_busy_ms_per_step", 0.0), 4),
+                            "kernel_ms_per_step": pst.get("kernel_ms_per_step"),
+                            "source": "FETCH_SIZE x 2 + WRITE_SIZE summed over the timed window's dispatches "
+                                      "(bench.py's markers, %d steps) / steps, over this run's ms_per_step; "
+                                      "busy = union of the window's kernel intervals / steps (%s)"
+                                      % (pst["steps"], pst.get("source", "profiles/pmc_step.json"))}
+    if pst and pst.get("per_step", {}).get("SQ_INSTS_VALU") and "issue_bound" in out:
+        ps = pst["per_step"]
+        rate = ps["SQ_INSTS_VALU"] / (ms_per_step * 1e-3)
+        d = {"valu_insts_per_step": int(ps["SQ_INSTS_VALU"]), "achieved": round(rate / 1e9, 2),
+             "frac": round(rate / VALU_ISSUE_PEAK, 4)}
+        if ps.get("SQ_WAVE_CYCLES"):
+            d["wave_time_split"] = {k: round(ps[c] / ps["SQ_WAVE_CYCLES"], 4) for k, c in
+                                    (("issuing", "SQ_ACTIVE_INST_ANY"), ("waiting", "SQ_WAIT_ANY"),
+                                     ("issue_stalled", "SQ_WAIT_INST_ANY")) if c in ps}
+        d["source"] = "SQ counters summed over the timed window's dispatches / steps (profiles/pmc_step.json)"
+        out["issue_bound"]["per_step"] = d
+    if cam_path:
+        out["camera_path"] = {
+            "ms_per_step": round(cam_path[0] / args.steps * 1e3, 4), "steps": args.steps,
+            "Mrays_s": round(cam_path[1] / cam_path[0] / 1e6, 3), "rays_per_frame_mean": int(cam_path[1] / args.steps),
+            "move": "per frame: Camera::translate({0, 0, %g}) and rotate(Quat(up, %g) * Quat(right, 0)) -- main.cc's W "
+                    "key and a one-pixel mouse motion (main.cc:144-177)" % (MOVE_SPEED, ROT_SPEED),
+            "note": "same pipeline as the headline with the camera moved before every frame; rays from a counted "
+                    "replay of the same poses; value stays on the static headline camera (BASELINE config)"}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, scene_path)
     print(json.dumps(out), flush=True)

@@ -543,7 +543,7 @@ __device__ __forceinline__ bool ft_root_hit(const SceneView& S, const BvhRefs& b
 //    change Light::attenuate (light.cu:35-58).
 //  * triangle skip (cast_local's t_lo): a triangle whose plane crossing is certainly
 //    before tlo(leaf) - M cannot be accepted, so its inside test is not run.
-template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false, bool PROF = false>
+template <bool NOLEAF, bool STATS, bool FT = false, bool AXIS = false, bool PROF = false, bool BRUTE = false>
 __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& bv, bool active_in, const Ray& r,
                                             Best& b, WaveCounters& wc, float occl_t = -1.0f,
                                             float lim = INFINITY) {
@@ -558,7 +558,26 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
     const unsigned long long am = __ballot(active);
     if (STATS || PROF) { wc.rays += __popcll(am); wc.wq++; }
     bool hit = false;
-    if (!S.use_bvh || S.n_leaf == 0) {                         // brute force (scene.cu:48-52)
+    if (BRUTE) {
+        // Brute-force kernels (M_BRUTE; the reference's -r, scene.cu:48-52): every instance in
+        // ascending order, strict < on time, with no tree code compiled in (the traversal's
+        // registers and its second copy of the leaf code made config 2's kernel spill).  The
+        // triangles take the axis-plane path (AXIS: identity rotations) with no entry bound;
+        // a lane that found an occluding hit (occl_t, all-opaque scenes) stops.
+        DirPre pre{};
+        if (AXIS) pre = dir_pre<true>(r.d);
+        else if (S.ident_all) pre = dir_pre(r.d);
+        bool live = active;
+        for (int i = 0; i < S.n_inst; i++) {
+            if (!__ballot(live)) break;
+            if (live && cast_local<false, AXIS, PROF>(S, bv, i, r, b, pre, wc, -INFINITY)) {
+                hit = true;
+                if (b.time <= occl_t) live = false;
+            }
+        }
+        return hit;
+    }
+    if (!FT && (!S.use_bvh || S.n_leaf == 0)) {               // brute force (scene.cu:48-52)
         DirPre pre{};
         if (S.ident_all) pre = dir_pre(r.d);
         for (int i = 0; i < S.n_inst; i++) {
@@ -898,6 +917,31 @@ __device__ __forceinline__ int lane_id_fresh() {
     return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
 }
 
+// Lane -> (pixel, sample) of pixel group g, from the launch parameters (shifts for powers of
+// two).  Recomputed where each term is used (camera ray, hit-id and output stores) rather than
+// held in registers across the trace: the output pixel's index held across it was spilled to
+// scratch (a store per group and lane; brute-force frames at spp = 1 wrote ~12 B per pixel).
+struct GroupLane { int px, py, sub, base, pix; bool valid; };
+__device__ __forceinline__ GroupLane group_lane(int g) {
+    KTP& P = kparams();
+    const int L = P.lanes_per_px;
+    const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
+    const int ln = lane_id_fresh();
+    const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
+    const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
+    const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
+    GroupLane o;
+    o.sub = P.l_shift >= 0 ? ln & (L - 1) : ln - pix_g * L;
+    o.base = ln - o.sub;
+    o.px = gx * P.gw + pxo;
+    const int pr = gy * P.gh + pyo;
+    o.valid = pix_g < P.px_per_wave && o.px < P.W && pr < P.n_rows;
+    o.py = P.row0 + pr * P.row_step;
+    o.pix = P.compact ? pr * P.W + o.px : o.py * P.W + o.px;   // < 2^31 (checked on the host)
+    return o;
+}
+
+
 
 template <class PT>
 __device__ __forceinline__ void dbg(const PT& P, bool me, int ev) {
@@ -923,8 +967,8 @@ __device__ __forceinline__ Ray camera_at(const DCamera& c, float cx, float cy) {
 //   ST_LIGHT       illuminate(): set up the shadow ray of light `li` (phong.cu:42-53)
 //   ST_WAIT_SHADOW waiting for a shadow segment (Light::attenuate, light.cu:29-61)
 // The top frame lives in registers; frames suspended under a reflection child (at
-// most `depth`) in the private array `stk`.  out_p >= 0: this lane carries the
-// pixel's sample 0 and records the primary hit ids there.
+// most `depth`) in the private array `stk`.  rec_ids: this lane carries the pixel's
+// sample 0 and records the primary hit ids of its pixel in group g.
 enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_WAIT_SHADOW = 4 };
 
 // Parking (PARK): integrator state the traversal never reads is written to this lane's
@@ -942,9 +986,9 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // profiles/r04/ab_nn.log).
 constexpr int PARK_FIELDS = 29;
 __host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 25 : PARK_FIELDS; }
-template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false>
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false, bool BRUTE = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
-                                           Ray r0, bool me, int out_p, WaveCounters& wc, float* park, int& nq) {
+                                           Ray r0, bool me, bool rec_ids, int g, WaveCounters& wc, float* park, int& nq) {
     constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
     constexpr bool NN = PARK;                                   // is_nn parked across the queries
     KTP& P0 = kparams();
@@ -952,8 +996,9 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
     SavedFrame stk[NS > 0 ? NS : 1];
     int top = -1, st = ST_DONE;
     // bit 0: primary ray not yet answered; bit 1: pop after illumination (depth 0);
-    // bit 2: `cur` was resumed from stk[top] (hit point / normal live there)
-    int fl = 1;
+    // bit 2: `cur` was resumed from stk[top] (hit point / normal live there);
+    // bit 3: this lane records the pixel's primary hit ids (sample 0)
+    int fl = rec_ids ? 9 : 1;
     V4 acc = v4(0, 0, 0, 0);
     float is_time = INFINITY;                                   // the sample's shared Isect
     V3 is_norm = v3(0, 0, 0);
@@ -1108,7 +1153,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         // (an unlit-skipped shadow step, max_t = -inf, takes no query)
         const bool qa = st == ST_WAIT_NORMAL || (st == ST_WAIT_SHADOW && max_t >= 0.0f);
         const unsigned long long prof_p0 = wc.wpair, prof_l0 = wc.wleaf;
-        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF>(SV(), bv, qa, q, b, wc, occl, lim);
+        const bool hit = closest_hit<false, STATS, FT, AXIS, PROF, BRUTE>(SV(), bv, qa, q, b, wc, occl, lim);
         if (PROF && P.stats) {                                 // query occupancy (rt_frame_work)
             const unsigned long long mp = __ballot(st == ST_WAIT_NORMAL && (fl & 1));
             const unsigned long long mn = __ballot(st == ST_WAIT_NORMAL);
@@ -1160,9 +1205,8 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         if (st == ST_WAIT_NORMAL) {
             if (fl & 1) {
                 fl &= ~1;
-                if (out_p >= 0) {
-                    int op = out_p;
-                    opaque(op);
+                if (fl & 8) {                                  // the pixel of group g, recomputed here
+                    const int op = group_lane(g).pix;
                     if (P.hit_inst) P.hit_inst[op] = hit ? b.inst : -1;
                     if (P.hit_tri) P.hit_tri[op] = hit ? b.tri : -1;
                 }
@@ -1237,8 +1281,9 @@ __host__ __device__ inline size_t shade_bytes(const SceneView& S) {
     return a16(sizeof(DMat) * (size_t)S.n_mats) + a16(sizeof(DLight) * (size_t)S.n_lights) +
            a16(sizeof(DTri) * (size_t)S.n_tris) + a16(sizeof(DMesh) * (size_t)S.n_meshes);
 }
-__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false) {
+__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false, bool brute = false) {
     const size_t sh = shade ? shade_bytes(S) : 0;
+    if (brute) return a16(16 * (size_t)S.n_inst) + sh;        // inst4 only (M_BRUTE)
     if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
     return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
 }
@@ -1254,20 +1299,25 @@ template <class T> __device__ __forceinline__ const T* stage_words(unsigned char
 
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
-template <bool LDS, bool FT = false, bool SHADE = false>
+template <bool LDS, bool FT = false, bool SHADE = false, bool BRUTE = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
     bv.fnode = S.fnode;
     bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
     bv.mats = S.mats; bv.lights = S.lights; bv.tris = S.tris; bv.meshes = S.meshes;
     if (LDS && SHADE) {                                    // after the BVH image (lds_bytes without the cache)
-        unsigned char* p = smem + lds_bytes(S, FT);
+        unsigned char* p = smem + lds_bytes(S, FT, false, BRUTE);
         bv.mats = stage_words(p, S.mats, S.n_mats);       p += a16(sizeof(DMat) * (size_t)S.n_mats);
         bv.lights = stage_words(p, S.lights, S.n_lights); p += a16(sizeof(DLight) * (size_t)S.n_lights);
         bv.tris = stage_words(p, S.tris, S.n_tris);       p += a16(sizeof(DTri) * (size_t)S.n_tris);
         bv.meshes = stage_words(p, S.meshes, S.n_meshes);
     }
-    if (LDS && FT) {                                       // ordered LBVH | inst4
+    if (LDS && BRUTE) {                                    // inst4 (no tree)
+        float4* in = reinterpret_cast<float4*>(smem);
+        for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
+        __syncthreads();
+        bv.inst = in;
+    } else if (LDS && FT) {                                // ordered LBVH | inst4
         const int nf = 4 * (S.n_real - 1);
         const float4* src = S.fnode;
         float4* fn = reinterpret_cast<float4*>(smem);
@@ -1310,25 +1360,29 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // MODE bit 5 (AXIS): FT with the axis-plane triangle path (S.tri_ax, cast_local).
 // MODE bit 6 (PROF): profiling variant of the fast kernel -- wave-level step counts and
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
-constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128;
+// MODE bit 8 (BRUTE): brute-force frames (use_bvh = 0) with only the instance loop compiled
+// (closest_hit); LDS image = inst4 (+ the shading cache, parking area).
+constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128,
+              M_BRUTE = 256;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     (void)P_arg;                                               // read in place: kparams()
     KTP& P = kparams();
     constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
-    constexpr bool SHADE = (MODE & M_SHADE) != 0;
-    const BvhRefs bv = stage_bvh<LDS, FT, SHADE>(S, smem);
+    constexpr bool SHADE = (MODE & M_SHADE) != 0, BRUTE = (MODE & M_BRUTE) != 0;
+    static_assert(!(BRUTE && FT), "a brute-force kernel has no tree");
+    const BvhRefs bv = stage_bvh<LDS, FT, SHADE, BRUTE>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
-    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE)) + threadIdx.x : nullptr;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE, BRUTE)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     if (PROF) {                                                // this wave's occupancy counters (zeroed)
-        wc.pc = reinterpret_cast<unsigned long long*>(smem + lds_bytes(S, FT, SHADE) +
+        wc.pc = reinterpret_cast<unsigned long long*>(smem + lds_bytes(S, FT, SHADE, BRUTE) +
                                                        (PARK ? (size_t)park_fields(NS) * 4 * TRACE_BLOCK_P : 0)) +
                 (threadIdx.x >> 6) * PROF_WAVE_SLOTS;
         if (lane < PROF_WAVE_SLOTS) wc.pc[lane] = 0;
@@ -1439,18 +1493,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             continue;
         const unsigned long long g_start = P.hist == 1 ? __builtin_amdgcn_s_memrealtime() : 0;
         int nq = 0;                                            // wave queries of this group (hist = 2)
-        const int gy = (int)udiv((unsigned)g, kld(P.div_ngx)), gx = g - gy * P.n_gx;
-        // lane -> (pixel, sample) terms recomputed per group by shifts (powers of two), not
-        // kept live across the trace
-        const int ln = lane_id_fresh();
-        const int pix_g = P.l_shift >= 0 ? ln >> P.l_shift : ln / L;
-        const int pxo = P.gw_shift >= 0 ? pix_g & (P.gw - 1) : pix_g % P.gw;
-        const int pyo = P.gw_shift >= 0 ? pix_g >> P.gw_shift : pix_g / P.gw;
-        const int sub_g = P.l_shift >= 0 ? ln & (L - 1) : ln - pix_g * L, base_g = ln - sub_g;
-        const int px = gx * P.gw + pxo, pr = gy * P.gh + pyo;
-        const bool valid = pix_g < P.px_per_wave && px < P.W && pr < P.n_rows;
-        const int py = P.row0 + pr * P.row_step;
-        const int pix_index = P.compact ? pr * P.W + px : py * P.W + px;   // < 2^31 (checked on the host)
+        const GroupLane gl = group_lane(g);
+        const int sub_g = gl.sub, px = gl.px, py = gl.py;
+        const bool valid = gl.valid;
         const bool me = valid && sub_g == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
@@ -1475,8 +1520,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // outputs are zeros (and -1 hit ids).  Most groups of the reference scenes are sky.
             if (FT && !STATS && !PROF && !MULTI && SV().use_bvh && SV().n_leaf > 0 && !kparams().gsky && !__ballot(ft_root_hit(SV(), bv, act, r0))) {
                 if (act && k == 0) {
-                    int op = pix_index;
-                    opaque(op);
+                    const int op = gl.pix;
                     if (P.hit_inst) P.hit_inst[op] = -1;
                     if (P.hit_tri) P.hit_tri[op] = -1;
                 }
@@ -1486,7 +1530,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // test); occupancy counters are taken over live groups' queries only
             if (PROF && FT) wc.live = __ballot(ft_root_hit(SV(), bv, act, r0)) != 0;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF>(S, bv, act, r0, me && rd == 0, (act && k == 0) ? pix_index : -1, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF, BRUTE>(S, bv, act, r0, me && rd == 0, act && k == 0, g, wc,
                                                  park, nq);
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
@@ -1501,21 +1545,21 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             KTP& Pr = kparams();
             const bool want_r = Pr.radiance != nullptr;
             const int spp_n = Pr.spp;
-            int bb = base_g;
-            opaque(bb);
+            const GroupLane ga = group_lane(g);                // after the trace (not held across it)
+            const int bb = ga.base, sub_a = ga.sub;
             const V4 cc = clamp1(c);
             if (L == 8) {                               // spp = 8: all permutes in one LDS round trip
                 V4 v[8];
 #pragma unroll
                 for (int s = 0; s < 8; s++) v[s] = shfl4(cc, bb + s);
-                if (sub_g == 0)
+                if (sub_a == 0)
 #pragma unroll
                     for (int s = 0; s < 8; s++)
                         if (rd * L + s < spp_n) sum_c = sum_c + v[s];
                 if (want_r) {
 #pragma unroll
                     for (int s = 0; s < 8; s++) v[s] = shfl4(c, bb + s);
-                    if (sub_g == 0)
+                    if (sub_a == 0)
 #pragma unroll
                         for (int s = 0; s < 8; s++)
                             if (rd * L + s < spp_n) sum_r = sum_r + v[s];
@@ -1523,19 +1567,19 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             } else {
                 for (int s = 0; s < L; s++) {
                     const V4 v = shfl4(cc, bb + s);
-                    if (sub_g == 0 && rd * L + s < spp_n) sum_c = sum_c + v;
+                    if (sub_a == 0 && rd * L + s < spp_n) sum_c = sum_c + v;
                 }
                 if (want_r)
                     for (int s = 0; s < L; s++) {
                         const V4 v = shfl4(c, bb + s);
-                        if (sub_g == 0 && rd * L + s < spp_n) sum_r = sum_r + v;
+                        if (sub_a == 0 && rd * L + s < spp_n) sum_r = sum_r + v;
                     }
             }
         }
-        if (valid && sub_g == 0) {
+        const GroupLane go = group_lane(g);                    // the output pixel, recomputed here
+        if (go.valid && go.sub == 0) {
             KTP& P = kparams();
-            int p = pix_index;
-            opaque(p);                                         // address math stays here, not live across the trace
+            const int p = go.pix;
             const float inv = (float)P.spp;
             // mean = sum / spp (raytracer.cu's per-sample colour, build-defined spp average);
             // for spp = 2^k, x * 2^-k is the same correctly rounded value as x / 2^k
@@ -2727,7 +2771,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     if (!s->work_zeroed) HIPCHK(hipMemsetAsync(s->d_work, 0, WORK_INTS * sizeof(int), st));
     const bool tex = o.textures != 0;
     const int mode0 = (o.spp > 64 ? M_MULTI : 0) | (want_stats ? M_STATS : 0);
-    const bool ft = mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
+    // brute force (the reference's -r): no tree kernel (closest_hit's FT path assumes a tree)
+    const bool brute = !S.use_bvh || S.n_leaf == 0;
+    const bool ft = !brute && mode0 == 0 && S.ftree && lds_bytes(S, true) <= (size_t)LDS_LIMIT;
     const size_t lds = lds_bytes(S, ft);
     const bool use_lds = lds <= (size_t)LDS_LIMIT;
     // suspended frames needed (<= MAX_FRAMES - 1); none without a refractive material, where a
@@ -2752,7 +2798,15 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // LDS shading cache beside the parked main kernel (not with the profiling variant)
     const bool shade = park && ft && S.tri_ax && !prof &&
                        lds + shade_bytes(S) + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    if (tex && ft) {                                           // textured fast frames: ordered LBVH, unparked
+    // brute-force fast frames: the instance loop only (M_BRUTE), axis-plane triangles, parked
+    // state and the LDS shading cache beside the instance records
+    const size_t lds_br = lds_bytes(S, false, true, true);
+    const bool brute_k = brute && !tex && mode == 0 && !prof && S.tri_ax && lds_br + park_bytes <= (size_t)PARK_LDS_LIMIT;
+    if (brute_k) {
+        constexpr int BR = M_BRUTE | M_PARK | M_SHADE | M_AXIS;
+        fn = ns <= 0 ? (const void*)trace_kernel<0, true, BR> : ns <= 2 ? (const void*)trace_kernel<2, true, BR>
+                                                               : (const void*)trace_kernel<NG, true, BR>;
+    } else if (tex && ft) {                                    // textured fast frames: ordered LBVH, unparked
         constexpr int TF = M_TEX | M_FT, TA = M_TEX | M_FT | M_AXIS;
         fn = S.tri_ax ? (ns <= 2 ? (const void*)trace_kernel<2, true, TA> : (const void*)trace_kernel<NG, true, TA>)
                       : (ns <= 2 ? (const void*)trace_kernel<2, true, TF> : (const void*)trace_kernel<NG, true, TF>);
@@ -2782,8 +2836,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0) +
-                       (prof ? PROF_LDS_BYTES : 0);
+    const size_t shm = brute_k ? lds_br + park_bytes
+                               : (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0) +
+                                     (prof ? PROF_LDS_BYTES : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     int per_cu = 1;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, TRACE_BLOCK_P, shm) != hipSuccess || per_cu < 1) per_cu = 1;
@@ -2802,12 +2857,15 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // optional second half of the grid gated on later frames being queued
     // (profiles/r03/ab_grid/readback.log): such callers set RT_OVERLAP_FULL.
     int cap = s->n_cu * per_cu;
+    // another frame of the scene still in flight (any slot count, any overlap policy): the heavy
+    // list's static dealing below is for frames whose blocks all start at once
+    bool other_running = false;
+    for (int i = 1; i < s->n_slots && !other_running; i++) {
+        const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
+        other_running = s->slot_pending[sl] && hipEventQuery(s->slot_done[sl]) == hipErrorNotReady;
+    }
     if (s->n_slots >= 4 && s->overlap != RT_OVERLAP_FULL) {
-        bool running = s->overlap == RT_OVERLAP_STREAM;        // another frame of the scene in flight, or a stream
-        for (int i = 1; i < s->n_slots && !running; i++) {
-            const int sl = (s->cur_slot + s->n_slots - i) % s->n_slots;
-            running = s->slot_pending[sl] && hipEventQuery(s->slot_done[sl]) == hipErrorNotReady;
-        }
+        const bool running = s->overlap == RT_OVERLAP_STREAM || other_running;   // or a stream
         // Small frames (row slices of N >= 4 ranks: under ~48 groups per wave on half the CUs)
         // take a quarter: four frames' blocks share the GPU, each block runs twice the groups,
         // so its LDS staging and its slowest wave's tail weigh half as much.  Measured per-rank
@@ -2823,7 +2881,9 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     int blocks = std::min(cap, (waves_needed + TRACE_BLOCK_P / 64 - 1) / (TRACE_BLOCK_P / 64));
     blocks = std::max(blocks, 1);
     P.grid_waves = blocks * (TRACE_BLOCK_P / 64);              // the launch below: dim3(blocks)
-    P.heavy_static = blocks == s->n_cu * per_cu ? 1 : 0;       // every block starts at once (no frame running)
+    // every block starts at once: a full grid and no other frame of the scene running (RT_OVERLAP_FULL
+    // and 2-3 frame slots keep the full grid for overlapping frames; those frames keep the counter)
+    P.heavy_static = (blocks == s->n_cu * per_cu && !other_running) ? 1 : 0;
     P.heavy_cap = std::max(2 * blocks * (TRACE_BLOCK_P / 64), P.n_groups / 4);   // a bound, not a target
     // longest-first history (fast frames): valid while the launch layout is unchanged
     // Only where a wave runs few groups (1080p 8-way row slices: ~8 per wave): with more (63
@@ -3261,6 +3321,21 @@ int rt_set_device(int device) {
     return RT_OK;
 }
 
+// Profile marker (rt_profile_marker): an empty kernel whose grid (64 x tag threads) tells a
+// rocprofv3 trace where a caller's timed region begins and ends (tools/pmc_step.py).
+namespace {
+__global__ __launch_bounds__(64) void profile_marker_kernel(int tag) { (void)tag; }
+}  // namespace
+
+int rt_profile_marker(int tag, void* stream) {
+    if (tag < 1 || tag > 64) return fail(RT_ERR_ARG, "marker tag must be 1..64");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    hipLaunchKernelGGL(profile_marker_kernel, dim3(tag), dim3(64), 0, (hipStream_t)stream, tag);
+    HIPCHK(hipGetLastError());
+    return RT_OK;
+}
+
 int rt_spp_offset(int k, float* dx, float* dy) {
     if (k < 0 || !dx || !dy) return fail(RT_ERR_ARG, "bad arguments");
     rt::spp_offset(k, dx, dy);
@@ -3396,9 +3471,26 @@ int rt_scene_info(const rt_scene* s, int32_t* c) {
     return RT_OK;
 }
 
+// (ABI 3) hit_tri indexes the triangles in flattened mesh order, so the meshes must list every
+// triangle exactly once: a bitmap of the triangles seen, failing on a repeat or on one left out
+// (a count alone would pass a list that repeats one triangle and omits another).
+static bool meshes_cover_tris_once(const rt::Scene& h) {
+    std::vector<unsigned char> seen(h.tris.size(), 0);
+    size_t n = 0;
+    for (auto& m : h.meshes)
+        for (int i : m.tris) {
+            if (i < 0 || (size_t)i >= seen.size() || seen[i]) return false;
+            seen[i] = 1;
+            n++;
+        }
+    return n == h.tris.size();
+}
+
 int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
     CHECK_FINISHED(s);
     const rt::Scene& h = s->h;
+    if ((what == RT_EXPORT_TRIS || what == RT_EXPORT_TEXCOORDS) && !meshes_cover_tris_once(h))
+        return fail(RT_ERR_STATE, "meshes do not cover every triangle once");
     std::vector<float> f;
     std::vector<int32_t> iv;
     switch (what) {
@@ -3407,8 +3499,6 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
         case RT_EXPORT_TRIS:                                   // flattened (mesh) order: hit_tri indexes it
             for (auto& m : h.meshes)
                 for (int i : m.tris) { const auto& t = h.tris[i]; iv.insert(iv.end(), {t.i0, t.i1, t.i2, t.mat}); }
-            // (ABI 3) one record per triangle: the meshes list every triangle exactly once
-            if (iv.size() != 4 * h.tris.size()) return fail(RT_ERR_STATE, "meshes do not cover every triangle once");
             break;
         case RT_EXPORT_MATERIALS:
             for (auto& m : h.mats) {
@@ -3438,7 +3528,6 @@ int rt_scene_export(const rt_scene* s, int what, void* dst, int64_t cap) {
                     const auto& t = h.tris[i];
                     f.insert(f.end(), {(float)t.tex.has, t.tex.tx, t.tex.ty, t.tex.ux, t.tex.uy, t.tex.vx, t.tex.vy});
                 }
-            if (f.size() != 7 * h.tris.size()) return fail(RT_ERR_STATE, "meshes do not cover every triangle once");
             break;
         case RT_EXPORT_ATLAS: {
             const size_t n = h.atlas_rgba.size();

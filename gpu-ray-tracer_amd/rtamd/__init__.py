@@ -36,7 +36,7 @@ SYMBOLS = [
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
     "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_scene_set_overlap", "rt_frame_work",
-    "rt_scene_set_devices",
+    "rt_scene_set_devices", "rt_profile_marker",
 ]
 
 
@@ -139,6 +139,8 @@ def lib():
     L.rt_scene_set_overlap.argtypes = [vp, ip]
     L.rt_frame_work.argtypes = [vp, ctypes.POINTER(RenderOpts), ctypes.POINTER(Work)]
     L.rt_scene_set_devices.argtypes = [vp, vp, ip, ip]
+    if hasattr(L, "rt_profile_marker"):         # (absent from libraries older than ABI 3's round 5: A/B runs)
+        L.rt_profile_marker.argtypes = [ip, vp]
     _lib = L
     return L
 
@@ -173,6 +175,13 @@ def spp_offset(k):
     dx, dy = ctypes.c_float(), ctypes.c_float()
     _check(lib().rt_spp_offset(k, ctypes.byref(dx), ctypes.byref(dy)))
     return dx.value, dy.value
+
+
+def profile_marker(tag, stream=None):
+    """An empty marker kernel of `tag` workgroups on `stream` (an int hipStream_t, None = the
+    default stream): tools/pmc_step.py finds a timed region between two markers."""
+    if hasattr(lib(), "rt_profile_marker"):
+        _check(lib().rt_profile_marker(int(tag), stream))
 
 
 def material(Ke=(0, 0, 0, 0), Ka=(0, 0, 0, 0), Kd=(0, 0, 0, 0), Ks=(0, 0, 0, 0), Kt=(0, 0, 0, 0), Kr=(0, 0, 0, 0),

@@ -231,6 +231,11 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap);
 int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2,
                   float* out_f, int32_t* out_i, uint64_t* out_u);
 
+/* Profiling hook: launches an empty marker kernel of `tag` (1..64) workgroups on `stream` (a
+ * hipStream_t; NULL = the default stream), so a rocprofv3 kernel or counter trace can find the
+ * caller's timed region between two markers (bench.py --pmc-window, tools/pmc_step.py). */
+int rt_profile_marker(int tag, void* stream);
+
 /* Sample offset table of the build-defined spp extension (k=0 -> (0,0)). */
 int rt_spp_offset(int k, float* dx, float* dy);
 

@@ -65,8 +65,12 @@ template <class T> struct Quat {          // (i, j, k, r) as geometry.h:20-181
     T i = 0, j = 0, k = 0, r = 1;
     Quat() = default;
     Quat(T i_, T j_, T k_, T r_) : i(i_), j(j_), k(k_), r(r_) {}
+    // geometry.h:36-41 as a g++ translation unit compiles it (main.cc:175-176, cube_world.cc:173):
+    // unqualified cos / sin of the float 0.5f * theta resolve to the C double functions there,
+    // and the result is rounded to T.  std::cos(float) would round differently for some theta.
     Quat(Vec3<T> axis, T theta) {
-        const T hc = std::cos(0.5f * theta), hs = std::sin(0.5f * theta);
+        const T hc = static_cast<T>(::cos(static_cast<double>(0.5f * theta)));
+        const T hs = static_cast<T>(::sin(static_cast<double>(0.5f * theta)));
         i = axis[0] * hs; j = axis[1] * hs; k = axis[2] * hs; r = hc;
     }
     static Quat identity() { return Quat(); }
