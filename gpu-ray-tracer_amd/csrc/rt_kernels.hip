@@ -986,7 +986,13 @@ enum : int { ST_DONE = 0, ST_ADVANCE = 1, ST_WAIT_NORMAL = 2, ST_LIGHT = 3, ST_W
 // profiles/r04/ab_nn.log).
 constexpr int PARK_FIELDS = 29;
 __host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 25 : PARK_FIELDS; }
-template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false, bool BRUTE = false>
+// Partial parking (M_PART): scenes whose ordered tree fills most of the LDS (world16: 93 KB)
+// park the first PART_FIELDS fields only (the ray, its attenuation and the accumulated
+// radiance); the rest stay in registers.  The instance records are then read from global
+// memory (scalar loads: a leaf's instance is wave-uniform) to leave the LDS to the tree.
+constexpr int PART_FIELDS = 14;
+template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false, bool BRUTE = false,
+          bool PART = false>
 __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv, bool valid,
                                            Ray r0, bool me, bool rec_ids, int g, WaveCounters& wc, float* park, int& nq) {
     constexpr bool OPQ = NS == 0;                               // no refractive material in the scene
@@ -1138,7 +1144,7 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
         if (PARK) {
             float* pk = park;
             int f = 0;
-            auto put = [&](float v) { pk[(f++) * TRACE_BLOCK_P] = v; };
+            auto put = [&](float v) { if (!PART || f < PART_FIELDS) pk[f * TRACE_BLOCK_P] = v; f++; };
             put(cur.ray.o.x); put(cur.ray.o.y); put(cur.ray.o.z); put(cur.ray.d.x); put(cur.ray.d.y); put(cur.ray.d.z);
             put(cur.atten.x); put(cur.atten.y); put(cur.atten.z); put(cur.atten.w);
             put(acc.x); put(acc.y); put(acc.z); put(acc.w);
@@ -1181,15 +1187,15 @@ __device__ __forceinline__ V4 trace_sample(const SceneView& S, const BvhRefs& bv
             asm volatile("" ::: "memory");
             const float* pk = park;
             int f = 0;
-            auto get = [&]() { return pk[(f++) * TRACE_BLOCK_P]; };
-            cur.ray.o.x = get(); cur.ray.o.y = get(); cur.ray.o.z = get();
-            cur.ray.d.x = get(); cur.ray.d.y = get(); cur.ray.d.z = get();
-            cur.atten.x = get(); cur.atten.y = get(); cur.atten.z = get(); cur.atten.w = get();
-            acc.x = get(); acc.y = get(); acc.z = get(); acc.w = get();
-            summed.x = get(); summed.y = get(); summed.z = get(); summed.w = get();
-            fct.x = get(); fct.y = get(); fct.z = get(); fct.w = get();
-            if (NN) { is_nn.x = get(); is_nn.y = get(); is_nn.z = get(); }
-            if (!OPQ) { rv.x = get(); rv.y = get(); rv.z = get(); rv.w = get(); }
+            auto get = [&](float& x) { if (!PART || f < PART_FIELDS) x = pk[f * TRACE_BLOCK_P]; f++; };
+            get(cur.ray.o.x); get(cur.ray.o.y); get(cur.ray.o.z);
+            get(cur.ray.d.x); get(cur.ray.d.y); get(cur.ray.d.z);
+            get(cur.atten.x); get(cur.atten.y); get(cur.atten.z); get(cur.atten.w);
+            get(acc.x); get(acc.y); get(acc.z); get(acc.w);
+            get(summed.x); get(summed.y); get(summed.z); get(summed.w);
+            get(fct.x); get(fct.y); get(fct.z); get(fct.w);
+            if (NN) { get(is_nn.x); get(is_nn.y); get(is_nn.z); }
+            if (!OPQ) { get(rv.x); get(rv.y); get(rv.z); get(rv.w); }
             if (PROF) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); wc.cyc_park += __builtin_amdgcn_s_memtime() - cq1; }
         }
         unsigned long long c1 = 0;
@@ -1281,9 +1287,11 @@ __host__ __device__ inline size_t shade_bytes(const SceneView& S) {
     return a16(sizeof(DMat) * (size_t)S.n_mats) + a16(sizeof(DLight) * (size_t)S.n_lights) +
            a16(sizeof(DTri) * (size_t)S.n_tris) + a16(sizeof(DMesh) * (size_t)S.n_meshes);
 }
-__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false, bool brute = false) {
+__host__ __device__ inline size_t lds_bytes(const SceneView& S, bool ft = false, bool shade = false, bool brute = false,
+                                            bool part = false) {
     const size_t sh = shade ? shade_bytes(S) : 0;
     if (brute) return a16(16 * (size_t)S.n_inst) + sh;        // inst4 only (M_BRUTE)
+    if (ft && part) return 64 * (size_t)(S.n_real - 1) + sh;   // the ordered tree only (M_PART)
     if (ft) return 64 * (size_t)(S.n_real - 1) + 16 * (size_t)S.n_inst + sh;
     return a16(48 * (size_t)S.n_leaf + 4 * (size_t)S.n_leaf) + a16(16 * (size_t)S.n_inst) + sh;
 }
@@ -1299,14 +1307,14 @@ template <class T> __device__ __forceinline__ const T* stage_words(unsigned char
 
 // LDS image of a persistent block: node pairs [3n float4] | leaf_inst [n] | inst4 [n_inst]
 // (16-B aligned); lds_bytes() on the host must match.
-template <bool LDS, bool FT = false, bool SHADE = false, bool BRUTE = false>
+template <bool LDS, bool FT = false, bool SHADE = false, bool BRUTE = false, bool PART = false>
 __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* smem) {
     BvhRefs bv;
     bv.fnode = S.fnode;
     bv.pair = S.node_pair; bv.leaf = S.leaf_inst; bv.inst = S.inst4;
     bv.mats = S.mats; bv.lights = S.lights; bv.tris = S.tris; bv.meshes = S.meshes;
     if (LDS && SHADE) {                                    // after the BVH image (lds_bytes without the cache)
-        unsigned char* p = smem + lds_bytes(S, FT, false, BRUTE);
+        unsigned char* p = smem + lds_bytes(S, FT, false, BRUTE, PART);
         bv.mats = stage_words(p, S.mats, S.n_mats);       p += a16(sizeof(DMat) * (size_t)S.n_mats);
         bv.lights = stage_words(p, S.lights, S.n_lights); p += a16(sizeof(DLight) * (size_t)S.n_lights);
         bv.tris = stage_words(p, S.tris, S.n_tris);       p += a16(sizeof(DTri) * (size_t)S.n_tris);
@@ -1317,6 +1325,13 @@ __device__ __forceinline__ BvhRefs stage_bvh(const SceneView& S, unsigned char* 
         for (int i = threadIdx.x; i < S.n_inst; i += blockDim.x) in[i] = S.inst4[i];
         __syncthreads();
         bv.inst = in;
+    } else if (LDS && FT && PART) {                        // ordered LBVH (inst4 stays in global memory)
+        const int nf = 4 * (S.n_real - 1);
+        const float4* src = S.fnode;
+        float4* fn = reinterpret_cast<float4*>(smem);
+        for (int i = threadIdx.x; i < nf; i += blockDim.x) fn[i] = src[i];
+        __syncthreads();
+        bv.fnode = fn;
     } else if (LDS && FT) {                                // ordered LBVH | inst4
         const int nf = 4 * (S.n_real - 1);
         const float4* src = S.fnode;
@@ -1362,27 +1377,29 @@ __device__ __forceinline__ V4 shfl4(V4 v, int src) {
 // s_memtime cycle accounting (rt_experiment 6); results identical, timing perturbed.
 // MODE bit 8 (BRUTE): brute-force frames (use_bvh = 0) with only the instance loop compiled
 // (closest_hit); LDS image = inst4 (+ the shading cache, parking area).
+// MODE bit 9 (PART): partial parking (PART_FIELDS) with the tree alone in LDS (see PART_FIELDS).
 constexpr int M_MULTI = 1, M_STATS = 2, M_PARK = 4, M_TEX = 8, M_FT = 16, M_AXIS = 32, M_PROF = 64, M_SHADE = 128,
-              M_BRUTE = 256;
+              M_BRUTE = 256, M_PART = 512;
 template <int NS, bool LDS, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg, SceneView S) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     (void)P_arg;                                               // read in place: kparams()
     KTP& P = kparams();
     constexpr bool FT = (MODE & M_FT) != 0, AXIS = (MODE & M_AXIS) != 0;
-    constexpr bool SHADE = (MODE & M_SHADE) != 0, BRUTE = (MODE & M_BRUTE) != 0;
+    constexpr bool SHADE = (MODE & M_SHADE) != 0, BRUTE = (MODE & M_BRUTE) != 0, PART = (MODE & M_PART) != 0;
     static_assert(!(BRUTE && FT), "a brute-force kernel has no tree");
-    const BvhRefs bv = stage_bvh<LDS, FT, SHADE, BRUTE>(S, smem);
+    static_assert(!PART || (FT && (MODE & M_PARK)), "partial parking is a parked ordered-tree kernel");
+    const BvhRefs bv = stage_bvh<LDS, FT, SHADE, BRUTE, PART>(S, smem);
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
     constexpr bool PROF = (MODE & M_PROF) != 0, CYC = STATS || PROF;
     constexpr bool TEX = (MODE & M_TEX) != 0;
-    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE, BRUTE)) + threadIdx.x : nullptr;
+    float* park = PARK ? reinterpret_cast<float*>(smem + lds_bytes(S, FT, SHADE, BRUTE, PART)) + threadIdx.x : nullptr;
     const int rounds = MULTI ? (P.spp + L - 1) / L : 1;
     WaveCounters wc{0, 0, 0, 0};
     if (PROF) {                                                // this wave's occupancy counters (zeroed)
-        wc.pc = reinterpret_cast<unsigned long long*>(smem + lds_bytes(S, FT, SHADE, BRUTE) +
+        wc.pc = reinterpret_cast<unsigned long long*>(smem + lds_bytes(S, FT, SHADE, BRUTE, PART) +
                                                        (PARK ? (size_t)park_fields(NS) * 4 * TRACE_BLOCK_P : 0)) +
                 (threadIdx.x >> 6) * PROF_WAVE_SLOTS;
         if (lane < PROF_WAVE_SLOTS) wc.pc[lane] = 0;
@@ -1530,7 +1547,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // test); occupancy counters are taken over live groups' queries only
             if (PROF && FT) wc.live = __ballot(ft_root_hit(SV(), bv, act, r0)) != 0;
             const unsigned long long cs = CYC ? __builtin_amdgcn_s_memtime() : 0;
-            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF, BRUTE>(S, bv, act, r0, me && rd == 0, act && k == 0, g, wc,
+            V4 c = trace_sample<NS, STATS, PARK, TEX, FT, AXIS, PROF, BRUTE, PART>(S, bv, act, r0, me && rd == 0, act && k == 0, g, wc,
                                                  park, nq);
             if (CYC) wc.cyc_sample += __builtin_amdgcn_s_memtime() - cs;
             auto clamp1 = [](V4 v) {                           // raytracer.cu:37-40
@@ -2802,7 +2819,17 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     // state and the LDS shading cache beside the instance records
     const size_t lds_br = lds_bytes(S, false, true, true);
     const bool brute_k = brute && !tex && mode == 0 && !prof && S.tri_ax && lds_br + park_bytes <= (size_t)PARK_LDS_LIMIT;
-    if (brute_k) {
+    // ordered tree in LDS but no room for the whole parking area beside the instance records
+    // (world16: 93 KB tree + 23 KB instances): partial parking, instances from global memory
+    const size_t lds_pt = lds_bytes(S, true, true, false, true);
+    const size_t part_bytes = (size_t)PART_FIELDS * 4 * TRACE_BLOCK_P;
+    // (textured frames too: the hit's atlas colour stays in registers)
+    const bool part_k = !brute_k && ft && (!park || tex) && mode == 0 && !prof && S.tri_ax && ns <= 0 &&
+                        lds_pt + part_bytes <= (size_t)PARK_LDS_LIMIT && !getenv("RT_NO_PART");
+    if (part_k) {
+        constexpr int PT = M_PARK | M_FT | M_AXIS | M_SHADE | M_PART;
+        fn = tex ? (const void*)trace_kernel<0, true, PT | M_TEX> : (const void*)trace_kernel<0, true, PT>;
+    } else if (brute_k) {
         constexpr int BR = M_BRUTE | M_PARK | M_SHADE | M_AXIS;
         fn = ns <= 0 ? (const void*)trace_kernel<0, true, BR> : ns <= 2 ? (const void*)trace_kernel<2, true, BR>
                                                                : (const void*)trace_kernel<NG, true, BR>;
@@ -2836,7 +2863,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     } else if (mode != 0 || ns > 2) fn = generic[use_lds ? 1 : 0][mode];
     else if (use_lds) fn = ns <= 0 ? (const void*)trace_kernel<0, true, 0> : (const void*)trace_kernel<2, true, 0>;
     else fn = ns <= 0 ? (const void*)trace_kernel<0, false, 0> : (const void*)trace_kernel<2, false, 0>;
-    const size_t shm = brute_k ? lds_br + park_bytes
+    const size_t shm = part_k ? lds_pt + part_bytes : brute_k ? lds_br + park_bytes
                                : (park ? lds + park_bytes : use_lds ? lds : 0) + (shade ? shade_bytes(S) : 0) +
                                      (prof ? PROF_LDS_BYTES : 0);
     if (shm > 64 * 1024) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

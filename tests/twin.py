@@ -49,10 +49,26 @@ def orc_render(oracle, orc_scene, **kw):
     return oracle.render(orc_scene, **kw)
 
 
-def assert_frames_equal(gpu_fr, orc_fr, keys=("rgba", "radiance", "hit_inst", "hit_tri"), rtol=1e-5, ctx=""):
+def _record_pm1(ctx, n, total):
+    """Log the observed count of +-1 RGBA bytes per comparison (gpurun_out/rgba_pm1.jsonl) so
+    that the BASELINE configs' assertions can quote the exact count (tests/test_gpu_fullsize.py)."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(root, "gpurun_out", "rgba_pm1.jsonl"), "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "ctx": str(ctx),
+                                "pm1_bytes": int(n), "bytes": int(total)}) + "\n")
+    except OSError:
+        pass
+
+
+def assert_frames_equal(gpu_fr, orc_fr, keys=("rgba", "radiance", "hit_inst", "hit_tri"), rtol=1e-5, ctx="",
+                        max_pm1=None):
     """The parity bar (BASELINE north_star): hit ids bit-exact, radiance within 1e-5 relative,
-    RGBA8 bytes within 1 where a 1-ulp radiance difference (pow) crosses a byte boundary, on
-    fewer than 1e-3 of the bytes."""
+    RGBA8 bytes within 1 where a 1-ulp radiance difference (pow) crosses a byte boundary: at most
+    `max_pm1` such bytes (the count observed at that configuration, tests/test_gpu_fullsize.py),
+    or, where no count is recorded, fewer than 1e-3 of the bytes."""
     for k in ("hit_inst", "hit_tri"):
         if k in keys:
             assert np.array_equal(gpu_fr[k], orc_fr[k]), (ctx, k, int((gpu_fr[k] != orc_fr[k]).sum()))
@@ -65,5 +81,10 @@ def assert_frames_equal(gpu_fr, orc_fr, keys=("rgba", "radiance", "hit_inst", "h
         ga = np.ascontiguousarray(gpu_fr["rgba"]).view(np.uint8).astype(int)
         oa = np.ascontiguousarray(orc_fr["rgba"]).view(np.uint8).astype(int)
         d = np.abs(ga - oa)
+        n = int((d > 0).sum())
+        _record_pm1(ctx, n, d.size)
         assert d.max() <= 1, (ctx, int(d.max()))
-        assert (d > 0).mean() < 1e-3, (ctx, float((d > 0).mean()))
+        if max_pm1 is not None:
+            assert n <= max_pm1, (ctx, n, max_pm1)
+        else:
+            assert (d > 0).mean() < 1e-3, (ctx, float((d > 0).mean()))
