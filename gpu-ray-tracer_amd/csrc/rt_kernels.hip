@@ -2074,6 +2074,43 @@ __global__ void kat_kernel(int op, int n, const float* a, const float* b, const 
             oi[i] = bx[6] != 0 && box_hit_f(L3(bx), L3(bx + 3), r, ray_inv(r));
             break;
         }
+        case 18: case 19: {   // box_from_local (create_boxes' from_local) / box_merge (the level merges)
+            const float* x = a + 7 * i;
+            const float* y = b + 7 * i;
+            Box bx; bx.mn = L3(x); bx.mx = L3(x + 3); bx.nd = x[6] != 0;
+            Box r;
+            if (op == 18) {
+                const Q o{y[0], y[1], y[2], y[3]};
+                Pose e;
+                e.p = L3(y + 4);
+                e.identity = __float_as_uint(o.i) == 0u && __float_as_uint(o.j) == 0u && __float_as_uint(o.k) == 0u &&
+                             __float_as_uint(o.r) == 0x3f800000u;
+                e.tn = qnormalized(o); e.ti = qinverse(o);
+                const Q inv = qinverse(o);
+                e.fn = qnormalized(inv); e.fi = qinverse(inv);
+                r = from_local(bx, e);
+            } else {
+                Box by; by.mn = L3(y); by.mx = L3(y + 3); by.nd = y[6] != 0;
+                r = merge(bx, by);
+            }
+            S3(of + 6 * i, r.mn); S3(of + 6 * i + 3, r.mx); oi[i] = r.nd ? 1 : 0;
+            break;
+        }
+        case 20: {   // entity pose transforms (cast_local / Hitable::hit pose chain)
+            const float* y = a + 7 * i;
+            const Q o{y[0], y[1], y[2], y[3]};
+            Pose e;
+            e.p = L3(y + 4);
+            e.identity = __float_as_uint(o.i) == 0u && __float_as_uint(o.j) == 0u && __float_as_uint(o.k) == 0u &&
+                         __float_as_uint(o.r) == 0x3f800000u;
+            e.tn = qnormalized(o); e.ti = qinverse(o);
+            const Q inv = qinverse(o);
+            e.fn = qnormalized(inv); e.fi = qinverse(inv);
+            const V3 v = L3(b + 3 * i);
+            S3(of + 12 * i, point_to_local(e, v)); S3(of + 12 * i + 3, vec_to_local(e, v));
+            S3(of + 12 * i + 6, point_from_local(e, v)); S3(of + 12 * i + 9, vec_from_local(e, v));
+            break;
+        }
         case 16: of[i] = rcp_cr(a[i]); break;                   // device CR reciprocal (rt_math.h)
         case 17: of[i] = sqrt_cr(a[i]); break;                  // device CR sqrt
         case 15: {   // packed child-pair box test (pair_hit): two boxes (mn, mx, nd) x 2 vs one ray
@@ -4005,13 +4042,14 @@ int rt_kat_device(const char* op, int n, const float* in0, const float* in1, con
                   uint64_t* ou) {
     static const char* ops[] = {"normalize3", "cross", "reflect", "refract", "quat_rotate", "quat_inverse", "quat_mul",
                                 "tri_hit", "ray_ctor", "zorder", "to_mat3", "box_hit", "pow", "tri_hit_f", "box_hit_f",
-                                "box_pair", "rcp_cr", "sqrt_cr"};
+                                "box_pair", "rcp_cr", "sqrt_cr", "box_from_local", "box_merge", "entity"};
     // per-op sizes (floats): in0, in1, in2, out_f, out_i, out_u per element
     static const int sz[][6] = {{3, 0, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 0, 3, 0, 0}, {3, 3, 2, 3, 1, 0},
                                 {4, 3, 0, 3, 0, 0}, {4, 0, 0, 4, 0, 0}, {4, 4, 0, 4, 0, 0}, {9, 6, 0, 3, 1, 0},
                                 {6, 0, 0, 6, 0, 0}, {3, 0, 0, 0, 0, 1}, {4, 0, 0, 9, 0, 0}, {7, 6, 0, 0, 1, 0},
                                 {1, 1, 0, 1, 0, 0}, {9, 6, 0, 3, 1, 0}, {7, 6, 0, 0, 1, 0}, {14, 6, 0, 0, 2, 0},
-                                {1, 0, 0, 1, 0, 0}, {1, 0, 0, 1, 0, 0}};
+                                {1, 0, 0, 1, 0, 0}, {1, 0, 0, 1, 0, 0}, {7, 7, 0, 6, 1, 0}, {7, 7, 0, 6, 1, 0},
+                                {7, 3, 0, 12, 0, 0}};
     if (!op || n <= 0) return fail(RT_ERR_ARG, "bad arguments");
     int k = -1;
     for (int i = 0; i < (int)(sizeof ops / sizeof *ops); i++) if (!strcmp(op, ops[i])) k = i;

@@ -451,7 +451,8 @@ def kat_device(op, *inputs):
              "quat_rotate": (3, 0, 0), "quat_inverse": (4, 0, 0), "quat_mul": (4, 0, 0), "tri_hit": (3, 1, 0),
              "ray_ctor": (6, 0, 0), "zorder": (0, 0, 1), "to_mat3": (9, 0, 0), "box_hit": (0, 1, 0), "pow": (1, 0, 0),
              "tri_hit_f": (3, 1, 0), "box_hit_f": (0, 1, 0), "box_pair": (0, 2, 0),
-             "rcp_cr": (1, 0, 0), "sqrt_cr": (1, 0, 0)}
+             "rcp_cr": (1, 0, 0), "sqrt_cr": (1, 0, 0), "box_from_local": (6, 1, 0), "box_merge": (6, 1, 0),
+             "entity": (12, 0, 0)}
     nf, ni, nu = sizes[op]
     ins = [_f(a) for a in inputs] + [None] * (3 - len(inputs))
     n = inputs[0].shape[0]

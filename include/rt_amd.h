@@ -226,7 +226,9 @@ int rt_debug_cast(rt_scene* s, int x, int y, char* buf, int64_t cap);
 
 /* Device-side math known-answer entry (test hook): evaluates `op` element-wise on
  * the GPU.  op names as in oracle/rt_oracle.h's orc_kat_*, plus the filtered variants
- * tri_hit_f, box_hit_f and box_pair (two boxes per element, two int results).
+ * tri_hit_f, box_hit_f and box_pair (two boxes per element, two int results), and
+ * box_from_local / box_merge (box7 = min3 max3 nondegenerate; entity7 = quat4 pos3 -> box6 +
+ * int) and entity (entity7, v3 -> point/vec to/from local, 12 floats). 
  * Host pointers in/out. */
 int rt_kat_device(const char* op, int n, const float* in0, const float* in1, const float* in2,
                   float* out_f, int32_t* out_i, uint64_t* out_u);

@@ -1,8 +1,12 @@
 // kat_driver.cpp — known-answer harness over the REFERENCE's own math sources.
 //
 // Compiled (oracle/Makefile target `ref`) with g++ directly against the
-// reference's headers include/raymath/{linear.h,geometry.h} and its translation
-// unit src/rayopt/z_order.cu, unmodified, read in place from /root/reference.
+// reference's headers include/raymath/{linear.h,geometry.h}, include/rayopt/bounding_box.h,
+// include/rayprimitives/entity.h and its translation units src/rayopt/z_order.cu,
+// src/rayopt/bounding_box.cu and src/rayprimitives/entity.cu, unmodified, read in place from
+// /root/reference.  entity.h includes <cuda.h> / <cuda_runtime.h>: those are the CUDA 12.8
+// toolkit headers this image ships (Triton's copy, CUDA_INC in the Makefile), used as they
+// are -- under g++ they only declare the host runtime, and nothing here calls or links it.
 // Output binary: oracle/_ref/kat_ref (git-ignored).  It reads raw little-endian
 // input arrays and writes raw outputs; tests/golden/make_golden.py drives it and
 // commits the (inputs, outputs) pairs as fixtures.
@@ -28,6 +32,8 @@ using std::pow;
 #include "raymath/linear.h"
 #include "raymath/geometry.h"
 #include "rayopt/z_order.h"
+#include "rayopt/bounding_box.h"        // + src/rayopt/bounding_box.cu (slab test, from_local, merge)
+#include "rayprimitives/entity.h"       // + src/rayprimitives/entity.cu (pose transforms)
 
 using V3 = rmath::Vec3<float>;
 using V4 = rmath::Vec4<float>;
@@ -96,6 +102,38 @@ int main(int argc, char** argv) {
             put3(of, ray.origin()); put3(of, ray.direction());
         } else if (op == "zorder") {
             ou.push_back((uint64_t)ropt::z_order(v3(F(in, 3 * i))));
+        } else if (op == "box_hit") {              // BoundingBox::intersects (bounding_box.cu:62-104)
+            const float* b = F(in, 7 * i);
+            const float* r = F(in, 7 * n + 6 * i);
+            ropt::BoundingBox bx;
+            bx.min = v3(b); bx.max = v3(b + 3); bx.nondegenerate = b[6] != 0;
+            R ray(v3(r), v3(r + 3));
+            float t = NAN;
+            const bool h = bx.intersects(ray, t);
+            of.push_back(h ? t : NAN);
+            oi.push_back(h ? 1 : 0);
+        } else if (op == "box_from_local" || op == "box_merge") {   // bounding_box.cu:5-60
+            const float* a = F(in, 7 * i);
+            const float* c = F(in, 7 * n + 7 * i);
+            ropt::BoundingBox ba;
+            ba.min = v3(a); ba.max = v3(a + 3); ba.nondegenerate = a[6] != 0;
+            ropt::BoundingBox r;
+            if (op == "box_from_local") {
+                rprimitives::Entity e(v3(c + 4), Q(c[0], c[1], c[2], c[3]));   // entity = (quat i j k r, pos)
+                r = ropt::from_local(ba, e);
+            } else {
+                ropt::BoundingBox bb;
+                bb.min = v3(c); bb.max = v3(c + 3); bb.nondegenerate = c[6] != 0;
+                r = ropt::merge(ba, bb);
+            }
+            put3(of, r.min); put3(of, r.max);
+            oi.push_back(r.nondegenerate ? 1 : 0);
+        } else if (op == "entity") {               // Entity point/vec to/from local (entity.cu:5-37)
+            const float* c = F(in, 7 * i);
+            const V3 v = v3(F(in, 7 * n + 3 * i));
+            rprimitives::Entity e(v3(c + 4), Q(c[0], c[1], c[2], c[3]));
+            put3(of, e.point_to_local(v)); put3(of, e.vec_to_local(v));
+            put3(of, e.point_from_local(v)); put3(of, e.vec_from_local(v));
         } else if (op == "axis_angle") {
             const float* a = F(in, 4 * i);
             V4 r = Q(v3(a), a[3]).to_Vec4();

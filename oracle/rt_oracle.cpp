@@ -1190,6 +1190,29 @@ void orc_kat_box_hit(int n, const float* b7, const float* r6, int32_t* hit, floa
         t[i] = tt;
     }
 }
+void orc_kat_box_from_local(int n, const float* b7, const float* e7, float* o6, int32_t* nd) {
+    for (int i = 0; i < n; i++) {
+        const float* b = b7 + 7 * i; const float* e = e7 + 7 * i;
+        Box r = from_local(Box{ld3(b), ld3(b + 3), b[6] != 0}, Entity{Quat{e[0], e[1], e[2], e[3]}, ld3(e + 4)});
+        st3(o6 + 6 * i, r.mn); st3(o6 + 6 * i + 3, r.mx); nd[i] = r.nd ? 1 : 0;
+    }
+}
+void orc_kat_box_merge(int n, const float* a7, const float* b7, float* o6, int32_t* nd) {
+    for (int i = 0; i < n; i++) {
+        const float* a = a7 + 7 * i; const float* b = b7 + 7 * i;
+        Box r = merge(Box{ld3(a), ld3(a + 3), a[6] != 0}, Box{ld3(b), ld3(b + 3), b[6] != 0});
+        st3(o6 + 6 * i, r.mn); st3(o6 + 6 * i + 3, r.mx); nd[i] = r.nd ? 1 : 0;
+    }
+}
+void orc_kat_entity(int n, const float* e7, const float* v3, float* o12) {
+    for (int i = 0; i < n; i++) {
+        const float* e = e7 + 7 * i;
+        const Entity en{Quat{e[0], e[1], e[2], e[3]}, ld3(e + 4)};
+        const V3 v = ld3(v3 + 3 * i);
+        st3(o12 + 12 * i, point_to_local(en, v)); st3(o12 + 12 * i + 3, vec_to_local(en, v));
+        st3(o12 + 12 * i + 6, point_from_local(en, v)); st3(o12 + 12 * i + 9, vec_from_local(en, v));
+    }
+}
 void orc_kat_axis_angle(int n, const float* a4, float* o) {
     for (int i = 0; i < n; i++) { Quat q = qaxis_angle_g(ld3(a4 + 4 * i), a4[4 * i + 3]); o[4 * i] = q.i; o[4 * i + 1] = q.j; o[4 * i + 2] = q.k; o[4 * i + 3] = q.r; }
 }

@@ -109,6 +109,9 @@ void orc_kat_quat_mul(int n, const float* a, const float* b, float* out);
 void orc_kat_tri_hit(int n, const float* tri9, const float* ray6, int32_t* hit, float* t_uv3); /* ray built with Ray(o,d) */
 void orc_kat_box_hit(int n, const float* box7, const float* ray6, int32_t* hit, float* t);
 void orc_kat_zorder(int n, const float* v, uint64_t* out);
+void orc_kat_box_from_local(int n, const float* box7, const float* entity7, float* out6, int32_t* nd);  /* from_local */
+void orc_kat_box_merge(int n, const float* a7, const float* b7, float* out6, int32_t* nd);              /* merge */
+void orc_kat_entity(int n, const float* entity7, const float* v3, float* out12);  /* Entity p/v to/from local */
 void orc_kat_axis_angle(int n, const float* axis_theta4, float* out);          /* Quat(axis, theta), g++-TU cos/sin */
 void orc_kat_to_mat3(int n, const float* q, float* out9);
 void orc_kat_ray_ctor(int n, const float* ray6, float* out6);                   /* Ray(o,d): normalizes d */

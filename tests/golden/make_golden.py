@@ -5,8 +5,8 @@ Two families:
 
 1. ``kat_<op>.npz`` — known-answer vectors for the math primitives on the hot
    path, produced by ``oracle/_ref/kat_ref``: the REFERENCE's own
-   include/raymath/{linear.h,geometry.h} and src/rayopt/z_order.cu compiled
-   unmodified with g++ (``make -C oracle ref``).  Inputs are seeded numpy draws
+   include/raymath/{linear.h,geometry.h}, src/rayopt/{z_order,bounding_box}.cu and
+   src/rayprimitives/entity.cu compiled unmodified with g++ (``make -C oracle ref``).  Inputs are seeded numpy draws
    concentrated on the numerically delicate regions (grazing rays, triangle
    edges, tiny vectors under the 1e-5 threshold, signed zeros).
 
@@ -138,6 +138,56 @@ def make_kats():
         print("kat", k, {kk: vv.shape for kk, vv in dct.items()})
 
 
+def _adv_boxes(rng, n):
+    """Boxes with rays aimed at points near them, dense on faces, edges and corners (the slab
+    test's ties), zero direction components, degenerate boxes, negative-zero coordinates."""
+    mn = (rng.normal(size=(n, 3)) * 4).astype(np.float32)
+    mx = (mn + np.abs(rng.normal(size=(n, 3))) + np.float32(1e-3)).astype(np.float32)
+    mx[: n // 16] = mn[: n // 16]                                 # flat / point boxes
+    nd = (rng.random((n, 1)) < 0.95).astype(np.float32)
+    box = np.concatenate([mn, mx, nd], 1).astype(np.float32)
+    o = (rng.normal(size=(n, 3)) * 20).astype(np.float32)
+    t = rng.uniform(-0.05, 1.05, size=(n, 3)).astype(np.float32)
+    snap = rng.random((n, 3))
+    t[snap < 0.3] = 0.0
+    t[(snap >= 0.3) & (snap < 0.6)] = 1.0
+    tgt = (mn + (mx - mn) * t).astype(np.float32)
+    d = (tgt - o).astype(np.float32)
+    d[rng.random((n, 3)) < 0.04] = 0.0
+    d[rng.random((n, 3)) < 0.01] = -0.0
+    inside = rng.random(n) < 0.05                                  # origins inside the box
+    o[inside] = ((mn + mx) * np.float32(0.5))[inside]
+    return box, np.concatenate([o, d], 1).astype(np.float32)
+
+
+def make_kats_geometry():
+    """Round 5: the slab test (BoundingBox::intersects), from_local / merge (create_boxes and the
+    BVH level merges) and the Entity pose transforms (cast_local, Hitable::hit), from the
+    reference's bounding_box.cu / entity.cu compiled unmodified with g++ (oracle/Makefile ref)."""
+    rng = np.random.default_rng(20261018)
+    out = {}
+    n = 8192
+    box, ray = _adv_boxes(rng, n)
+    of, oi, _ = _run("box_hit", n, [box, ray], n_f=n, n_i=n)
+    out["box_hit"] = dict(box=box, ray=ray, t=of, hit=oi)
+    q = _quats(rng, N)
+    q[N // 4: N // 2] = [0, 0, 0, 1]                              # the cube world's identity poses
+    ent = np.concatenate([q, _vecs(rng, N, (-1, 3))], 1).astype(np.float32)
+    b0, _ = _adv_boxes(rng, N)
+    of, oi, _ = _run("box_from_local", N, [b0, ent], n_f=6 * N, n_i=N)
+    out["box_from_local"] = dict(box=b0, entity=ent, out=of.reshape(N, 6), nd=oi)
+    b1, _ = _adv_boxes(rng, N)
+    b1[: N // 8, :6] = b0[: N // 8, :6]                           # equal boxes / shared faces
+    of, oi, _ = _run("box_merge", N, [b0, b1], n_f=6 * N, n_i=N)
+    out["box_merge"] = dict(a=b0, b=b1, out=of.reshape(N, 6), nd=oi)
+    v = _vecs(rng, N, (-3, 3))
+    of, _, _ = _run("entity", N, [ent, v], n_f=12 * N)
+    out["entity"] = dict(entity=ent, v=v, out=of.reshape(N, 12))
+    for k, dct in out.items():
+        np.savez_compressed(os.path.join(HERE, f"kat_{k}.npz"), **dct)
+        print("kat", k, {kk: vv.shape for kk, vv in dct.items()})
+
+
 FRAMES = [  # (scene, w, h, use_bvh, spp, semantics)
     ("world1", 256, 256, 1, 1, 1),      # config 1: CPU path (raytracer.cc)
     ("world1", 256, 256, 1, 1, 0),
@@ -165,5 +215,7 @@ if __name__ == "__main__":
     what = sys.argv[1:] or ["kats", "frames"]
     if "kats" in what:
         make_kats()
+    if "kats" in what or "geometry" in what:
+        make_kats_geometry()
     if "frames" in what:
         make_frames()

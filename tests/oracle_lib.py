@@ -134,6 +134,15 @@ class Oracle:
             h = np.zeros(n, np.int32)
             L.orc_kat_tri_hit(n, P(arrs[0]), P(arrs[1]), h.ctypes.data_as(_i), P(o))
             return h, o
+        if op in ("box_from_local", "box_merge"):
+            o = np.zeros((n, 6), np.float32)
+            nd = np.zeros(n, np.int32)
+            getattr(L, "orc_kat_" + op)(n, P(arrs[0]), P(arrs[1]), P(o), nd.ctypes.data_as(_i))
+            return o, nd
+        if op == "entity":
+            o = np.zeros((n, 12), np.float32)
+            L.orc_kat_entity(n, P(arrs[0]), P(arrs[1]), P(o))
+            return o
         if op == "box_hit":
             t = np.zeros(n, np.float32)
             h = np.zeros(n, np.int32)

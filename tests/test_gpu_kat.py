@@ -31,6 +31,36 @@ def test_device_math_bit_exact(gpu, op, inputs):
     assert np.array_equal(_bits(out.reshape(ref.shape)), _bits(ref)), op
 
 
+def test_device_slab_tests_equal_reference(gpu, oracle):
+    """Every device box test (exact, filtered, packed pair) against the reference-built slab
+    test vectors (kat_box_hit.npz: bounding_box.cu:62-104 compiled from the reference)."""
+    k = g("box_hit")
+    box, ray = k["box"], k["ray"]
+    assert np.array_equal(gpu.kat_device("box_hit", box, ray), k["hit"])
+    assert np.array_equal(gpu.kat_device("box_hit_f", box, ray), k["hit"])
+    other = np.roll(box, 1, axis=0)
+    pair = gpu.kat_device("box_pair", np.concatenate([box, other], 1), ray)
+    assert np.array_equal(pair[:, 0], k["hit"])
+    ref1, _ = oracle.kat("box_hit", other, ray)             # the oracle: pinned to the same TU (test_oracle.py)
+    assert np.array_equal(pair[:, 1], ref1)
+
+
+@pytest.mark.parametrize("op,inputs", [("box_from_local", ["box", "entity"]), ("box_merge", ["a", "b"])])
+def test_device_boxes_equal_reference(gpu, op, inputs):
+    """The BVH build's box arithmetic (rt_math.h from_local / merge, run by bvh_build_kernel)
+    against the reference-built vectors (bounding_box.cu:5-60)."""
+    k = g(op)
+    out, nd = gpu.kat_device(op, *[k[i] for i in inputs])
+    assert np.array_equal(nd, k["nd"])
+    assert np.array_equal(_bits(out), _bits(k["out"]))
+
+
+def test_device_entity_equal_reference(gpu):
+    """Pose transforms (rt_math.h Pose, identity specialisation included) against entity.cu."""
+    k = g("entity")
+    assert np.array_equal(_bits(gpu.kat_device("entity", k["entity"], k["v"])), _bits(k["out"]))
+
+
 def test_device_zorder(gpu):
     k = g("zorder")
     assert np.array_equal(gpu.kat_device("zorder", k["v"]), k["out"])

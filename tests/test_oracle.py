@@ -1,8 +1,8 @@
 """CPU tests: pin the oracle (test infrastructure) before trusting it.
 
 1. Math primitives: bit-exact against known-answer vectors produced by the
-   reference's own raymath headers / z_order.cu (tests/golden/kat_*.npz, made by
-   tests/golden/make_golden.py from oracle/_ref/kat_ref).
+   reference's own raymath headers, z_order.cu, bounding_box.cu and entity.cu
+   (tests/golden/kat_*.npz, made by tests/golden/make_golden.py from oracle/_ref/kat_ref).
 2. Whole-frame behaviour: ray / node / leaf / triangle counters and CPU-vs-GPU
    semantic image differences equal the measurements of the reference code
    recorded in SURVEY.md Appendix D and §8d.
@@ -50,6 +50,35 @@ def test_oracle_kat_triangle(oracle):
     assert np.array_equal(hit, g["hit"])
     assert np.array_equal(_bits(tuv), _bits(g["out"]))
     assert 0.2 < g["hit"].mean() < 0.9            # edge cases on both sides of the 1e-5 test
+
+
+def test_oracle_kat_slab_test(oracle):
+    """BoundingBox::intersects (bounding_box.cu:62-104) as the reference's own TU computes it
+    (kat_box_hit.npz, round 5): hit and entry time, on face / edge / corner targets, zero and
+    negative-zero direction components, flat and degenerate boxes, origins inside."""
+    g = golden("kat_box_hit.npz")
+    hit, t = oracle.kat("box_hit", g["box"], g["ray"])
+    assert np.array_equal(hit, g["hit"])
+    h = g["hit"] == 1
+    assert np.array_equal(_bits(t[h]), _bits(g["t"][h]))
+    assert 0.2 < g["hit"].mean() < 0.9
+
+
+@pytest.mark.parametrize("op,inputs", [("box_from_local", ["box", "entity"]), ("box_merge", ["a", "b"])])
+def test_oracle_kat_boxes(oracle, op, inputs):
+    """from_local (create_boxes' instance boxes) and merge (the BVH level merges),
+    bounding_box.cu:5-60, against the reference's TU."""
+    g = golden(f"kat_{op}.npz")
+    out, nd = oracle.kat(op, *[g[k] for k in inputs])
+    assert np.array_equal(nd, g["nd"])
+    assert np.array_equal(_bits(out), _bits(g["out"]))
+
+
+def test_oracle_kat_entity(oracle):
+    """Entity::point/vec_to/from_local (entity.cu:5-37): cast_local's and Hitable::hit's pose
+    chain, against the reference's TU."""
+    g = golden("kat_entity.npz")
+    assert np.array_equal(_bits(oracle.kat("entity", g["entity"], g["v"])), _bits(g["out"]))
 
 
 # SURVEY.md Appendix D: counters measured on the reference's GPU-semantics path (1080p, spp=1)
