@@ -2,8 +2,9 @@
 //
 // Compiled (oracle/Makefile target `ref`) with g++ directly against the
 // reference's headers include/raymath/{linear.h,geometry.h}, include/rayopt/bounding_box.h,
-// include/rayprimitives/entity.h and its translation units src/rayopt/z_order.cu,
-// src/rayopt/bounding_box.cu and src/rayprimitives/entity.cu, unmodified, read in place from
+// include/rayprimitives/{entity.h,gpu/hitable.cuh} and its translation units
+// src/rayopt/z_order.cu, src/rayopt/bounding_box.cu, src/rayprimitives/entity.cu and
+// src/rayprimitives/hitable.cu, unmodified, read in place from
 // /root/reference.  entity.h includes <cuda.h> / <cuda_runtime.h>: those are the CUDA 12.8
 // toolkit headers this image ships (Triton's copy, CUDA_INC in the Makefile), used as they
 // are -- under g++ they only declare the host runtime, and nothing here calls or links it.
@@ -34,6 +35,20 @@ using std::pow;
 #include "rayopt/z_order.h"
 #include "rayopt/bounding_box.h"        // + src/rayopt/bounding_box.cu (slab test, from_local, merge)
 #include "rayprimitives/entity.h"       // + src/rayprimitives/entity.cu (pose transforms)
+
+// Hitable::hit (hitable.cu:29-38) around a known local hit: a subclass whose hit_local (the
+// virtual the reference's Trimesh implements, trimesh.cu:11-19) records the local ray it is
+// given and reports a hit at a given local time and normal.
+#include "rayprimitives/gpu/hitable.cuh"
+struct KatHitable : rprimitives::gpu::Hitable {
+    rmath::Ray<float> seen;
+    float t_local = 0;
+    rmath::Vec3<float> n_local;
+    KatHitable(rmath::Vec3<float> p, rmath::Quat<float> o) : Hitable(p, o), seen(rmath::Vec3<float>(), rmath::Vec3<float>()) {}
+    bool hit_local(const rmath::Ray<float>& lr, renv::gpu::Scene*, rprimitives::Isect& is) override {
+        seen = lr; is.time = t_local; is.norm = n_local; return true;
+    }
+};
 
 using V3 = rmath::Vec3<float>;
 using V4 = rmath::Vec4<float>;
@@ -134,6 +149,17 @@ int main(int argc, char** argv) {
             rprimitives::Entity e(v3(c + 4), Q(c[0], c[1], c[2], c[3]));
             put3(of, e.point_to_local(v)); put3(of, e.vec_to_local(v));
             put3(of, e.point_from_local(v)); put3(of, e.vec_from_local(v));
+        } else if (op == "hitable") {              // Hitable::hit / HitHandle (hitable.cu:7-38)
+            const float* c = F(in, 7 * i);
+            const float* r = F(in, 7 * n + 6 * i);
+            const float* h = F(in, 13 * n + 4 * i);
+            KatHitable e(v3(c + 4), Q(c[0], c[1], c[2], c[3]));
+            e.t_local = h[0]; e.n_local = v3(h + 1);
+            float time = INFINITY;
+            rprimitives::Isect is(time);
+            R ray(v3(r), v3(r + 3));
+            e.hit(ray, nullptr, is);
+            put3(of, e.seen.origin()); put3(of, e.seen.direction()); of.push_back(time); put3(of, is.norm);
         } else if (op == "axis_angle") {
             const float* a = F(in, 4 * i);
             V4 r = Q(v3(a), a[3]).to_Vec4();

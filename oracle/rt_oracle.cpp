@@ -611,13 +611,23 @@ bool tri_hit(const Ctx& x, int t, const Ray& lr, Isect& is) {               // t
     return false;
 }
 
-bool mesh_hit(const Ctx& x, const Mesh& m, const Ray& ray, Isect& is) {      // hitable.cu:7-38 (HitHandle)
-    float scale = len(vec_to_local(m.e, ray.d));
-    Ray lr = ray_to_local(m.e, ray);
-    bool hit = false;
-    for (int t = m.begin; t < m.begin + m.count; t++) hit |= tri_hit(x, t, lr, is);  // trimesh.cu:11-19
-    if (hit) { is.norm = normalized(vec_from_local(m.e, is.norm)); is.time *= scale; }
+// Hitable::hit (hitable.cu:7-38, HitHandle): the entity's local ray, hit_local, then the
+// normal and time brought back (fix_isect).  hit_local(lr, is) -> bool.
+template <class F>
+bool hitable_hit(const Entity& e, const Ray& ray, Isect& is, F&& hit_local) {
+    float scale = len(vec_to_local(e, ray.d));                                 // get_local_ray
+    Ray lr = ray_to_local(e, ray);
+    bool hit = hit_local(lr, is);
+    if (hit) { is.norm = normalized(vec_from_local(e, is.norm)); is.time *= scale; }   // fix_isect
     return hit;
+}
+
+bool mesh_hit(const Ctx& x, const Mesh& m, const Ray& ray, Isect& is) {
+    return hitable_hit(m.e, ray, is, [&](const Ray& lr, Isect& li) {
+        bool hit = false;
+        for (int t = m.begin; t < m.begin + m.count; t++) hit |= tri_hit(x, t, lr, li);   // trimesh.cu:11-19
+        return hit;
+    });
 }
 
 bool cast_local(const Ctx& x, const Ray& r, Isect& is, int ti) {            // scene.cu:27-40
@@ -1211,6 +1221,19 @@ void orc_kat_entity(int n, const float* e7, const float* v3, float* o12) {
         const V3 v = ld3(v3 + 3 * i);
         st3(o12 + 12 * i, point_to_local(en, v)); st3(o12 + 12 * i + 3, vec_to_local(en, v));
         st3(o12 + 12 * i + 6, point_from_local(en, v)); st3(o12 + 12 * i + 9, vec_from_local(en, v));
+    }
+}
+void orc_kat_hitable(int n, const float* e7, const float* ray6, const float* hit4, float* o10) {
+    for (int i = 0; i < n; i++) {
+        const float* e = e7 + 7 * i; const float* h = hit4 + 4 * i;
+        const Entity en{Quat{e[0], e[1], e[2], e[3]}, ld3(e + 4)};
+        Isect is{};
+        is.time = INFINITY;
+        Ray seen{};
+        hitable_hit(en, make_ray(ld3(ray6 + 6 * i), ld3(ray6 + 6 * i + 3)), is, [&](const Ray& lr, Isect& li) {
+            seen = lr; li.time = h[0]; li.norm = ld3(h + 1); return true;     // a local hit at (t, n)
+        });
+        st3(o10 + 10 * i, seen.o); st3(o10 + 10 * i + 3, seen.d); o10[10 * i + 6] = is.time; st3(o10 + 10 * i + 7, is.norm);
     }
 }
 void orc_kat_axis_angle(int n, const float* a4, float* o) {

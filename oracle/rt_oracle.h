@@ -112,6 +112,8 @@ void orc_kat_zorder(int n, const float* v, uint64_t* out);
 void orc_kat_box_from_local(int n, const float* box7, const float* entity7, float* out6, int32_t* nd);  /* from_local */
 void orc_kat_box_merge(int n, const float* a7, const float* b7, float* out6, int32_t* nd);              /* merge */
 void orc_kat_entity(int n, const float* entity7, const float* v3, float* out12);  /* Entity p/v to/from local */
+/* Hitable::hit's pose step (HitHandle) around a local hit (t, n): local ray 6, time, normal 3 */
+void orc_kat_hitable(int n, const float* entity7, const float* ray6, const float* hit4, float* out10);
 void orc_kat_axis_angle(int n, const float* axis_theta4, float* out);          /* Quat(axis, theta), g++-TU cos/sin */
 void orc_kat_to_mat3(int n, const float* q, float* out9);
 void orc_kat_ray_ctor(int n, const float* ray6, float* out6);                   /* Ray(o,d): normalizes d */

@@ -183,6 +183,13 @@ def make_kats_geometry():
     v = _vecs(rng, N, (-3, 3))
     of, _, _ = _run("entity", N, [ent, v], n_f=12 * N)
     out["entity"] = dict(entity=ent, v=v, out=of.reshape(N, 12))
+    # Hitable::hit's pose step around a local hit (hitable.cu:7-38): rays from _vecs, local hits
+    # at random times (zeros, tiny, large) with random normals (tiny ones under the threshold)
+    rr = np.concatenate([_vecs(rng, N, (-1, 2)), _vecs(rng, N, (-3, 1))], 1).astype(np.float32)
+    hit = np.concatenate([(10.0 ** rng.uniform(-6, 3, size=(N, 1))).astype(np.float32), _vecs(rng, N, (-7, 1))], 1)
+    hit[: N // 32, 0] = 0.0
+    of, _, _ = _run("hitable", N, [ent, rr, hit], n_f=10 * N)
+    out["hitable"] = dict(entity=ent, ray=rr, hit=hit.astype(np.float32), out=of.reshape(N, 10))
     for k, dct in out.items():
         np.savez_compressed(os.path.join(HERE, f"kat_{k}.npz"), **dct)
         print("kat", k, {kk: vv.shape for kk, vv in dct.items()})

@@ -139,6 +139,10 @@ class Oracle:
             nd = np.zeros(n, np.int32)
             getattr(L, "orc_kat_" + op)(n, P(arrs[0]), P(arrs[1]), P(o), nd.ctypes.data_as(_i))
             return o, nd
+        if op == "hitable":
+            o = np.zeros((n, 10), np.float32)
+            L.orc_kat_hitable(n, P(arrs[0]), P(arrs[1]), P(arrs[2]), P(o))
+            return o
         if op == "entity":
             o = np.zeros((n, 12), np.float32)
             L.orc_kat_entity(n, P(arrs[0]), P(arrs[1]), P(o))

@@ -81,6 +81,13 @@ def test_oracle_kat_entity(oracle):
     assert np.array_equal(_bits(oracle.kat("entity", g["entity"], g["v"])), _bits(g["out"]))
 
 
+def test_oracle_kat_hitable(oracle):
+    """Hitable::hit's HitHandle (hitable.cu:7-38: the mesh pose's local ray, then the normal and
+    time of a local hit brought back), against the reference's TU around a known local hit."""
+    g = golden("kat_hitable.npz")
+    assert np.array_equal(_bits(oracle.kat("hitable", g["entity"], g["ray"], g["hit"])), _bits(g["out"]))
+
+
 # SURVEY.md Appendix D: counters measured on the reference's GPU-semantics path (1080p, spp=1)
 APPENDIX_D = {
     ("world1", 0): (2084662, 0, 4169324, 50031888),
