@@ -109,7 +109,7 @@ def test_cli_textured_mode(oracle, tmp_path):
     rgba = oracle.render(o, spp=1, nthreads=8, want=("rgba",))["rgba"]
     exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
     got = _ppm_rgb(out)
-    assert np.abs(got.astype(int) - exp.astype(int)).max() <= 1 and (got != exp).mean() < 1e-3
+    assert np.array_equal(got, exp), int((got != exp).sum())
 
 
 @pytest.mark.parametrize("ranks", [2, 3, 8])
@@ -169,4 +169,4 @@ def test_cli_frames_in_flight(oracle, tmp_path, extra):
     rgba = o["rgba"]
     exp = np.stack([(rgba >> 24) & 255, (rgba >> 16) & 255, (rgba >> 8) & 255], -1).astype(np.uint8)
     got = _ppm_rgb(out)
-    assert np.abs(got.astype(int) - exp.astype(int)).max() <= 1 and (got != exp).mean() < 1e-3
+    assert np.array_equal(got, exp), int((got != exp).sum())

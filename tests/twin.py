@@ -49,42 +49,43 @@ def orc_render(oracle, orc_scene, **kw):
     return oracle.render(orc_scene, **kw)
 
 
-def _record_pm1(ctx, n, total):
-    """Log the observed count of +-1 RGBA bytes per comparison (gpurun_out/rgba_pm1.jsonl) so
-    that the BASELINE configs' assertions can quote the exact count (tests/test_gpu_fullsize.py)."""
+def _record_pm1(ctx, n, total, rad_ne=None, rad_err=None):
+    """Log the observed count of differing RGBA bytes (and radiance values) per comparison
+    (gpurun_out/rgba_pm1.jsonl).  Round 5's GPU suite logged 814 comparisons, every BASELINE
+    config at full size among them, with 0 differing bytes: the assertions are byte-exact."""
     import json
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     try:
         os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
         with open(os.path.join(root, "gpurun_out", "rgba_pm1.jsonl"), "a") as f:
             f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "ctx": str(ctx),
-                                "pm1_bytes": int(n), "bytes": int(total)}) + "\n")
+                                "pm1_bytes": int(n), "bytes": int(total), "radiance_ne": rad_ne,
+                                "radiance_max_rel": rad_err}) + "\n")
     except OSError:
         pass
 
 
 def assert_frames_equal(gpu_fr, orc_fr, keys=("rgba", "radiance", "hit_inst", "hit_tri"), rtol=1e-5, ctx="",
-                        max_pm1=None):
-    """The parity bar (BASELINE north_star): hit ids bit-exact, radiance within 1e-5 relative,
-    RGBA8 bytes within 1 where a 1-ulp radiance difference (pow) crosses a byte boundary: at most
-    `max_pm1` such bytes (the count observed at that configuration, tests/test_gpu_fullsize.py),
-    or, where no count is recorded, fewer than 1e-3 of the bytes."""
+                        max_pm1=0):
+    """The parity bar (BASELINE north_star): hit ids bit-exact, radiance within 1e-5 relative
+    (the float tolerance north_star states: pow_pos may differ from the double pow by 1 ulp),
+    RGBA8 bytes exact.  `max_pm1` (default 0) admits that many bytes off by one, for a caller
+    that documents why; no test passes one: every comparison of round 5's suite had 0."""
     for k in ("hit_inst", "hit_tri"):
         if k in keys:
             assert np.array_equal(gpu_fr[k], orc_fr[k]), (ctx, k, int((gpu_fr[k] != orc_fr[k]).sum()))
+    rad_ne = rad_err = None
     if "radiance" in keys:
         a, b = gpu_fr["radiance"].astype(np.float64), orc_fr["radiance"].astype(np.float64)
         err = np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
         err[a == b] = 0
+        rad_ne, rad_err = int((a != b).sum()), float(err.max()) if err.size else 0.0
         assert err.max() <= rtol, (ctx, float(err.max()))
     if "rgba" in keys:
         ga = np.ascontiguousarray(gpu_fr["rgba"]).view(np.uint8).astype(int)
         oa = np.ascontiguousarray(orc_fr["rgba"]).view(np.uint8).astype(int)
         d = np.abs(ga - oa)
         n = int((d > 0).sum())
-        _record_pm1(ctx, n, d.size)
+        _record_pm1(ctx, n, d.size, rad_ne, rad_err)
         assert d.max() <= 1, (ctx, int(d.max()))
-        if max_pm1 is not None:
-            assert n <= max_pm1, (ctx, n, max_pm1)
-        else:
-            assert (d > 0).mean() < 1e-3, (ctx, float((d > 0).mean()))
+        assert n <= max_pm1, (ctx, n, max_pm1)

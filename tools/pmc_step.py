@@ -77,7 +77,7 @@ def busy(root):
         tot += ce - cs
         by = collections.defaultdict(lambda: [0, 0])
         for r in w:
-            n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             by[n][0] += 1
             by[n][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         return {"busy_ns": tot, "span_ns": max(e for _, e in iv) - iv[0][0], "dispatches": len(w),
