@@ -222,6 +222,9 @@ struct BvhRefs {
 #ifndef RT_HEAVY_STATIC
 #define RT_HEAVY_STATIC 1    // frames issued alone: heavy-list tickets assigned statically (trace_kernel)
 #endif
+#ifndef RT_LDS_SUM
+#define RT_LDS_SUM 1         // spp >= 16 in parked kernels: per-channel in-order sample sums through LDS
+#endif
 #ifndef RT_TPC
 #define RT_TPC 3             // work indices claimed per ticket (trace_kernel's group loop) over all
                              // groups; 3 vs 2: -0.8% world8_stress, -1.3% world8 (profiles/r01/ab_tpc_v33.log)
@@ -1390,6 +1393,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
     static_assert(!(BRUTE && FT), "a brute-force kernel has no tree");
     static_assert(!PART || (FT && (MODE & M_PARK)), "partial parking is a parked ordered-tree kernel");
     const BvhRefs bv = stage_bvh<LDS, FT, SHADE, BRUTE, PART>(S, smem);
+    // LDS-staged sample sums (spp >= 16) in the partially parked kernels (config 5's world16 at
+    // 64 spp); compiled out of the fully parked headline kernel, whose registers it would crowd
+    constexpr bool LSUM = RT_LDS_SUM && PART;
     const int lane = threadIdx.x & 63;
     const int L = P.lanes_per_px;
     constexpr bool MULTI = (MODE & M_MULTI) != 0, STATS = (MODE & M_STATS) != 0, PARK = (MODE & M_PARK) != 0;
@@ -1515,6 +1521,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         const bool valid = gl.valid;
         const bool me = valid && sub_g == 0 && px == P.dbg_x && py == P.dbg_y;
         V4 sum_c = v4(0, 0, 0, 0), sum_r = v4(0, 0, 0, 0);
+        float acc = 0.0f;                                      // RT_LDS_SUM: this lane's (pixel, channel) sum
         const unsigned long long g_t0 = CYC ? __builtin_amdgcn_s_memrealtime() : 0, g_q0 = wc.wq;
         const unsigned long long g_p0 = wc.wpair, g_l0 = wc.wleaf, g_r0 = wc.wtri;
         const unsigned long long g_c0 = wc.cyc_q, g_c1 = wc.cyc_leaf, g_c2 = wc.cyc_sample, g_c3 = wc.cyc_post;
@@ -1581,6 +1588,29 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                         for (int s = 0; s < 8; s++)
                             if (rd * L + s < spp_n) sum_r = sum_r + v[s];
                 }
+            } else if (LSUM && L >= 16) {
+                // spp >= 16 (whole waves, or 16-32 lanes, per pixel): the in-order sums run one per
+                // lane and channel through the wave's own parking columns (free between queries),
+                // a ds_read and an add per sample, instead of four ds_bpermutes, four adds and the
+                // leader's select per sample.  Lane j = (pixel p, channel f): channels 0-3 the
+                // clamped colour, 4-7 the raw radiance when requested; the same adds in k order.
+                const int ln = lane_id_fresh();                // (not held across the group loop)
+                float* wcol = park - ln;                       // the wave's column 0, field 0
+                float* mine = park;
+                mine[0] = cc.x; mine[TRACE_BLOCK_P] = cc.y; mine[2 * TRACE_BLOCK_P] = cc.z; mine[3 * TRACE_BLOCK_P] = cc.w;
+                if (want_r) {
+                    mine[4 * TRACE_BLOCK_P] = c.x; mine[5 * TRACE_BLOCK_P] = c.y;
+                    mine[6 * TRACE_BLOCK_P] = c.z; mine[7 * TRACE_BLOCK_P] = c.w;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int nsh = want_r ? 3 : 2;                // log2 of the channels per pixel
+                const int pj = ln >> nsh, fj = ln & ((1 << nsh) - 1);
+                const int n_s = min(L, spp_n - rd * L);        // samples of this round (uniform)
+                if (pj < kparams().px_per_wave) {
+                    const float* src = wcol + fj * TRACE_BLOCK_P + pj * L;
+                    for (int s = 0; s < n_s; s++) acc = acc + src[s];
+                }
+                __builtin_amdgcn_wave_barrier();
             } else {
                 for (int s = 0; s < L; s++) {
                     const V4 v = shfl4(cc, bb + s);
@@ -1592,6 +1622,18 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                         if (sub_a == 0 && rd * L + s < spp_n) sum_r = sum_r + v;
                     }
             }
+        }
+        if (LSUM && L >= 16) {                 // the channel sums to their pixel's leader
+            const int ln = lane_id_fresh();
+            float* wcol = park - ln;
+            const int nsh = kparams().radiance != nullptr ? 3 : 2;
+            const int pj = ln >> nsh, fj = ln & ((1 << nsh) - 1);
+            if (pj < kparams().px_per_wave) wcol[fj * TRACE_BLOCK_P + pj * L] = acc;
+            __builtin_amdgcn_wave_barrier();
+            const float* mine = park;
+            sum_c = v4(mine[0], mine[TRACE_BLOCK_P], mine[2 * TRACE_BLOCK_P], mine[3 * TRACE_BLOCK_P]);
+            if (nsh == 3) sum_r = v4(mine[4 * TRACE_BLOCK_P], mine[5 * TRACE_BLOCK_P], mine[6 * TRACE_BLOCK_P], mine[7 * TRACE_BLOCK_P]);
+            __builtin_amdgcn_wave_barrier();
         }
         const GroupLane go = group_lane(g);                    // the output pixel, recomputed here
         if (go.valid && go.sub == 0) {
