@@ -1608,7 +1608,12 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
                 const int n_s = min(L, spp_n - rd * L);        // samples of this round (uniform)
                 if (pj < kparams().px_per_wave) {
                     const float* src = wcol + fj * TRACE_BLOCK_P + pj * L;
-                    for (int s = 0; s < n_s; s++) acc = acc + src[s];
+                    int s = 0;
+                    for (; s + 4 <= n_s; s += 4) {             // 16-B reads (pj * L: a multiple of 16 floats)
+                        const float4 v = *reinterpret_cast<const float4*>(src + s);
+                        acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+                    }
+                    for (; s < n_s; s++) acc = acc + src[s];
                 }
                 __builtin_amdgcn_wave_barrier();
             } else {
