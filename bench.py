@@ -83,11 +83,14 @@ def parse():
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
     p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
-    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "stream"),
-                   choices=("stream", "half", "full", "last-full"),
-                   help="grid of the timed frames (rt_scene_set_overlap): stream = half the CUs for every frame, "
+    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "stream-last-full"),
+                   choices=("stream", "half", "full", "last-full", "stream-last-full"),
+                   help="grid of the timed frames (rt_scene_set_overlap): stream-last-full (default) = stream, "
+                        "with the timed region's last frame on every CU (no frame follows it: -3%% at 20 steps, "
+                        "DESIGN.md 4.1); stream = half the CUs for every frame, "
                         "the first included (RT_OVERLAP_STREAM); half = half the CUs for a frame issued while "
-                        "another runs; full = every CU; last-full = half except the timed region's last frame")
+                        "another runs; full = every CU; last-full = half except the timed region's last frame; "
+                        "stream-last-full = stream except the timed region's last frame (every CU)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
@@ -284,13 +287,13 @@ def main():
     torch.cuda.synchronize()
     if overlap and args.grid == "full":
         scene.set_overlap(True)
-    if overlap and args.grid == "stream":
+    if overlap and args.grid in ("stream", "stream-last-full"):
         scene.set_overlap(False, stream=True)               # the timed frames are issued back to back
     rtamd.profile_marker(1, stream.cuda_stream)             # the timed window starts (tools/pmc_step.py)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if overlap and args.grid == "last-full" and i == args.steps - 1:
+        if overlap and args.grid in ("last-full", "stream-last-full") and i == args.steps - 1:
             scene.set_overlap(True)                         # nothing is issued behind the last frame
         step(not args.no_kernel_timing and not overlap)
     fb.finish()                                             # the last frame's gather + un-permute
@@ -334,11 +337,13 @@ def main():
         torch.cuda.synchronize()
         if overlap and args.grid == "full":
             scene.set_overlap(True)
-        if overlap and args.grid == "stream":
+        if overlap and args.grid in ("stream", "stream-last-full"):
             scene.set_overlap(False, stream=True)
         tc0 = time.perf_counter()
         for i in range(args.steps):
             camera_move(scene)
+            if overlap and args.grid in ("last-full", "stream-last-full") and i == args.steps - 1:
+                scene.set_overlap(True)                     # as in the headline's timed loop
             step(False)
         fb.finish()
         torch.cuda.synchronize()
