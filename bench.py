@@ -544,6 +544,7 @@ def main():
         roof["per_step"] = {"traffic": int(b), "achieved": round(a, 2), "frac": round(a / HBM_PEAK_GBS, 5),
                             "traffic_over_algorithmic": round(b / max(1, algo_bytes), 2),
                             "gpu_busy_ms_per_step": round(pst.get("gpu_busy_ms_per_step", 0.0), 4),
+                            "profiled_ms_per_step": pst.get("profiled_ms_per_step"),
                             "kernel_ms_per_step": pst.get("kernel_ms_per_step"),
                             "source": "FETCH_SIZE x 2 + WRITE_SIZE summed over the timed window's dispatches "
                                       "(bench.py's markers, %d steps) / steps, over this run's ms_per_step; "

@@ -98,6 +98,11 @@ def main():
     if "FETCH_SIZE" in ps and "WRITE_SIZE" in ps:
         rd, wr = 2.0 * ps["FETCH_SIZE"] * 1024.0, ps["WRITE_SIZE"] * 1024.0
         entry.update(hbm_bytes_per_step=int(rd + wr), read_bytes_per_step=int(rd), write_bytes_per_step=int(wr))
+    kt_log = os.path.join(root, "kt.log")                 # the kernel-trace pass's own bench line
+    if os.path.exists(kt_log):
+        for line in open(kt_log):
+            if line.startswith("{") and '"ms_per_step"' in line:
+                entry["profiled_ms_per_step"] = json.loads(line)["ms_per_step"]
     if b:
         entry["gpu_busy_ms_per_step"] = b["busy_ns"] / steps / 1e6
         entry["window_span_ms"] = b["span_ns"] / 1e6
