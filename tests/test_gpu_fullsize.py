@@ -105,10 +105,12 @@ def test_world1_1080p_brute_force(gpu, oracle):
 
 
 @pytest.mark.parametrize("scene,textures", [("world16", False), ("world16_tex", True)])
-@pytest.mark.parametrize("spp", [64, 96])
+@pytest.mark.parametrize("spp", [16, 32, 48, 64, 96])
 def test_config5_sample_mapping(gpu, oracle, scene, textures, spp):
-    """Config 5 (world16, 64 spp, textured) at 320x180: the 64-lanes-per-pixel mapping and the
-    multi-round (spp > 64) kernels, fast and counted, against the oracle; counters too."""
+    """Config 5 (world16, 64 spp, textured) at 320x180: the 16/32/48/64-lanes-per-pixel mappings
+    and the multi-round (spp > 64) kernels, fast and counted, against the oracle; counters too.
+    spp 16-64 run the partially parked kernel's LDS-staged sample sums, with
+    (radiance requested) and without (RGBA only) the raw-radiance channel lanes."""
     w, h = 320, 180
     s = gpu.Scene.load_json(scene_path(scene), w, h)
     o = oracle.load(scene_path(scene), w, h)
@@ -126,6 +128,8 @@ def test_config5_sample_mapping(gpu, oracle, scene, textures, spp):
     fast = s.render(spp=spp, want=WANT, stats=False, textures=textures)
     for k in WANT:
         assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), k
+    only = s.render(spp=spp, want=("rgba",), stats=False, textures=textures)
+    assert np.array_equal(only["rgba"], full["rgba"])
     assert (full["hit_inst"] >= 0).mean() > 0.2
 
 
