@@ -569,7 +569,7 @@ def main():
                     "key and a one-pixel mouse motion (main.cc:144-177)" % (MOVE_SPEED, ROT_SPEED),
             "note": "same pipeline as the headline with the camera moved before every frame; rays from a counted "
                     "replay of the same poses; value stays on the static headline camera (BASELINE config)"}
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:       # the CPU baseline: rank 0 at N = 1 only
         out["cpu_baseline"] = cpu_baseline(args, scene_path)
     print(json.dumps(out), flush=True)
     if dist:
