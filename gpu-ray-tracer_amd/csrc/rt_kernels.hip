@@ -992,7 +992,7 @@ __host__ __device__ constexpr int park_fields(int ns) { return ns == 0 ? 25 : PA
 // Partial parking (M_PART): scenes whose ordered tree fills most of the LDS (world16: 93 KB)
 // park the first PART_FIELDS fields only (the ray, its attenuation and the accumulated
 // radiance); the rest stay in registers.  The instance records are then read from global
-// memory (scalar loads: a leaf's instance is wave-uniform) to leave the LDS to the tree.
+// memory (L2-resident; as scalar loads they measured +1%) to leave the LDS to the tree.
 constexpr int PART_FIELDS = 14;
 template <int NS, bool STATS, bool PARK, bool TEX, bool FT, bool AXIS, bool PROF = false, bool BRUTE = false,
           bool PART = false>
