@@ -825,6 +825,10 @@ struct TraceParams {
     // the tree's root -- its outputs are written already and the trace kernel skips it.
     // NULL: no pre-pass (the trace kernel runs the same test itself).
     const unsigned char* gsky;
+    // Brute-force frames (M_BRUTE): the sky pre-pass tests the instance boxes (mesh box +
+    // position) grown by sky_A + sky_B t instead of a tree's root (sky_brute = 1; see
+    // grown_box_maybe)
+    const Box* sky_mesh_box; int sky_brute; float sky_A, sky_B; int sky_pad_;
     // Live-group lists (sky_kernel): queue q's groups are live[q * live_cap + i] for i below
     // work[16 (NQ + 1 + q)], in arrival order.  NULL: queue q's groups are q + NQ j.
     const int* live; int live_cap;
@@ -1740,6 +1744,34 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
 // |D|), so every ray of the group takes the geometric slab test (no zero-axis skip and
 // no exact-path fallback for tiny components: ray_inv).  A group it does not decide gets
 // the exact per-ray root test.
+// Brute-force sky test.  In frames without a tree (the reference's -r,
+// scene.cu:48-52) every primary ray runs cast_local on every instance, and no box is tested.
+// With pure translations and zero mesh offsets (S.prune_abs >= 0) the distance-pruning claim
+// (closest_hit) bounds where an accepted hit can lie: a triangle of instance k is accepted at
+// world time t only at a point within prune_abs + 2^-13 t of its box (the claim's spatial
+// slack plus its time slack).  So when no t >= 0 puts the ray inside the box grown by A + B t
+// with A = 2 prune_abs, B = 2^-12 (twice that), no triangle of the instance is accepted.  The
+// interval of such t is formed in float: each bound's rounding (a few ulps of the scene radius
+// R and of t) is far below what the doubling adds (prune_abs >= 2^-14 R, and 2^-13 t), so an
+// interval found empty here is empty under the claim's slack.  Answers "maybe" unless empty.
+__device__ __forceinline__ bool grown_box_maybe(float4 lo, float4 hi, float A, float B, const Ray& r) {
+    float tl = 0.0f, th = INFINITY;
+    auto axis = [&](float l, float h, float o, float d) {
+        const float c1 = (l - A) - o, k1 = d + B;            // (d + B) t >= l - A - o
+        if (k1 > 0.0f) tl = fmaxf(tl, c1 / k1);
+        else if (k1 < 0.0f) th = fminf(th, c1 / k1);
+        else if (c1 > 0.0f) tl = INFINITY;
+        const float c2 = (h + A) - o, k2 = d - B;            // (d - B) t <= h + A - o
+        if (k2 > 0.0f) th = fminf(th, c2 / k2);
+        else if (k2 < 0.0f) tl = fmaxf(tl, c2 / k2);
+        else if (c2 < 0.0f) tl = INFINITY;
+    };
+    axis(lo.x, hi.x, r.o.x, r.d.x);
+    axis(lo.y, hi.y, r.o.y, r.d.y);
+    axis(lo.z, hi.z, r.o.z, r.d.z);
+    return !(tl > th);
+}
+
 __device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const SceneView& S, int g) {
     const DCamera& c = P.cam;
     if (!(c.near_ > 0.0f) || S.n_real < 2) return false;
@@ -1802,18 +1834,48 @@ __device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const Sce
 #endif
 constexpr int SKY_THREADS = 64 * RT_SKY_WAVES;
 static_assert(SKY_THREADS >= 128, "sky_kernel's heavy-list append uses threads 64..127");
+template <bool BRUTE>
 __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
     __shared__ unsigned long long s_sky, s_todo;
     __shared__ int s_cnt, s_base, s_list[64];
     __shared__ int s_hcnt, s_hbase, s_hlist[64];               // hist = 2: last frame's heavy groups
+    __shared__ float4 s_blo[64], s_bhi[64];                    // sky_brute: the instance boxes
     const bool h2 = P.hist == 2;
+    constexpr bool brute = BRUTE;                              // (host: P.sky_brute)
+    int nb = 0;
+    if (brute) {                                               // (uniform) instance k's box: mesh box + position
+        nb = S.n_inst;
+        if ((int)threadIdx.x < nb) {
+            const float4 I = S.inst4[threadIdx.x];
+            const Box mb = P.sky_mesh_box[__float_as_int(I.w) & 0x7fffffff];
+            s_blo[threadIdx.x] = mb.nd ? make_float4(mb.mn.x + I.x, mb.mn.y + I.y, mb.mn.z + I.z, 0.0f)
+                                       : make_float4(INFINITY, INFINITY, INFINITY, 0.0f);   // empty mesh: no hit
+            s_bhi[threadIdx.x] = mb.nd ? make_float4(mb.mx.x + I.x, mb.mx.y + I.y, mb.mx.z + I.z, 0.0f)
+                                       : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+        }
+        __syncthreads();
+    }
+    // does ray r (when act) possibly hit anything: the tree's root (the traversal's first step)
+    // or, in brute-force frames, some instance's grown box
+    auto root_hit = [&](bool act, const Ray& r) {
+        if constexpr (!BRUTE) {
+            BvhRefs bv{};
+            bv.fnode = S.fnode;
+            return ft_root_hit(S, bv, act, r);
+        }
+        if (!act) return false;
+        const float A = 2.0f * P.sky_A, B = P.sky_B;
+        for (int k = 0; k < nb; k++)
+            if (s_blo[k].x <= s_bhi[k].x && grown_box_maybe(s_blo[k], s_bhi[k], A, B, r)) return true;
+        return false;
+    };
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, L = P.lanes_per_px;
     const int base = blockIdx.x * 64;
     const int n_in = min(64, P.n_groups - base);
     if (wv == 0) {
         const int gl = base + lane;
         const bool in = lane < n_in;
-        const bool csky = in && cone_misses_root(P, S, gl);
+        const bool csky = in && !brute && cone_misses_root(P, S, gl);
         // Representative ray: a group the cone test leaves undecided is live as
         // soon as one of its primaries enters the root -- lane 0's (pixel 0, sample 0), the
         // trace kernel's own ray and test -- so only the groups whose representative misses
@@ -1823,9 +1885,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
             const int gy = (int)udiv((unsigned)gl, P.div_ngx), gx = gl - gy * P.n_gx;
             const float2 o = spp_offset_dev(0);
             const Ray rr = camera_at(P.cam, (float)(gx * P.gw) + o.x, (float)(P.row0 + gy * P.gh * P.row_step) + o.y);
-            BvhRefs bv{};
-            bv.fnode = S.fnode;
-            rlive = ft_root_hit(S, bv, true, rr);
+            rlive = root_hit(true, rr);
         }
         const unsigned long long m = __ballot(csky), t = __ballot(in && !csky && !rlive);
         if (csky) {
@@ -1892,9 +1952,7 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
             const float2 o = spp_offset_dev(sub_g);            // the trace kernel's own offsets
             r0 = camera_at(P.cam, (float)px + o.x, (float)py + o.y);
         }
-        BvhRefs bv{};
-        bv.fnode = S.fnode;
-        const bool sky = __ballot(ft_root_hit(S, bv, act, r0)) == 0;
+        const bool sky = __ballot(root_hit(act, r0)) == 0;
         if (lane == 0) {
             gsky[g] = sky ? 1 : 0;
             if (sky && P.hist == 1) P.hf_next[g] = 0;
@@ -3005,7 +3063,10 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
     P.hist = 0;
     const long long waves = (long long)blocks * (TRACE_BLOCK_P / 64);
     // sky pre-pass: the fast (ordered-LBVH) kernels, one round of samples, a tree to test
-    const bool sky = ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0;
+    // (brute-force frames: the instances' grown boxes instead, when the pruning claim holds)
+    const bool sky_brute = brute_k && !prof && !want_stats && o.spp <= 64 && S.prune_abs >= 0.0f && S.n_inst >= 1 &&
+                           S.n_inst <= 64 && !getenv("RT_NO_BRUTE_SKY");
+    const bool sky = (ft && !prof && o.spp <= 64 && S.use_bvh && S.n_leaf > 0) || sky_brute;
     // Heavy-first by work (hist = 2) where groups per wave are many: a group whose samples took
     // >= heavy_q wave queries (mirror pixels: primary, shadow and reflection chains) is flagged,
     // and the next frame of the slot runs the flagged groups first off a heavy live list the sky
@@ -3058,10 +3119,13 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         }
         P.gsky = s->d_gsky;
         P.live = s->d_live; P.live_cap = lcap;
+        P.sky_brute = sky_brute ? 1 : 0;
+        P.sky_mesh_box = s->d_mesh_box;
+        P.sky_A = S.prune_abs; P.sky_B = 0x1p-12f;
         if (s->n_slots > 1 && grew) { int r; if ((r = mirror_slot_caps(s)) != RT_OK) return r; }
         P.tpc = RT_TPC_LIVE;
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live};
-        HIPCHK(hipExtLaunchKernel((const void*)sky_kernel, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
+        HIPCHK(hipExtLaunchKernel(sky_brute ? (const void*)sky_kernel<true> : (const void*)sky_kernel<false>, dim3(sblocks), dim3(SKY_THREADS), sargs, 0, st, e0, nullptr, 0));
     }
     void* args[] = {&P, &S};
     HIPCHK(hipExtLaunchKernel(fn, dim3(blocks), dim3(TRACE_BLOCK_P), args, shm, st, sky ? nullptr : e0, e1, 0));

@@ -400,6 +400,49 @@ def test_sky_prepass_grazing_cones(gpu, oracle, spp, row_step):
     assert n > 60
 
 
+@pytest.mark.parametrize("scene,spp,row_step", [("world1", 1, 1), ("world1", 4, 3), ("world1", 16, 1)])
+def test_brute_sky_prepass_grazing(gpu, oracle, scene, spp, row_step):
+    """Brute-force frames (the reference's -r) with the sky pre-pass testing each instance's box
+    grown by the pruning slack (grown_box_maybe): cameras on, just beside
+    and away from every instance box's face planes, looking along them and across, so rays
+    pass within rounding of the grown boxes; fast frames (pre-pass) == counted frames (no
+    pre-pass) bit for bit and == the oracle's brute-force frames, whole frames and row slices."""
+    w, h = (64, 48) if spp <= 4 else (32, 24)
+    s = gpu.Scene.load_json(scene_path(scene), w, h)
+    o = oracle.load(scene_path(scene), w, h)
+    v = s.export("vertices")
+    inst = s.export("instances")
+    c, sn = np.cos, np.sin
+    quats = [(0.0, 0.0, 0.0, 1.0)]
+    for a in (0.25, 0.5, 1.0, 1.5):                            # about y (level views)
+        quats.append((0.0, float(sn(0.5 * np.pi * a)), 0.0, float(c(0.5 * np.pi * a))))
+    for a in (-0.25, 0.25):                                    # tilted down / up
+        quats.append((float(sn(0.5 * np.pi * a)), 0.0, 0.0, float(c(0.5 * np.pi * a))))
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    n = skies = 0
+    for i in range(min(len(inst), 3)):
+        lo, hi = inst[i, 4:7] + v.min(0), inst[i, 4:7] + v.max(0)
+        mid = 0.5 * (lo + hi)
+        for axis in range(3):
+            for side, plane in ((0, lo[axis]), (1, hi[axis])):
+                for off in (0.0, 1e-3, -1e-3, 2.0):
+                    pos = mid.copy()
+                    pos[axis] = plane + (off if side else -off)
+                    for q in quats[:: (1 if axis == 1 else 3)]:
+                        s.set_camera([float(x) for x in pos], q)
+                        kw = dict(spp=spp, use_bvh=False, want=want, row0=row_step - 1, row_step=row_step, compact=True)
+                        fast = s.render(stats=False, **kw)
+                        full = s.render(stats=True, **kw)
+                        for k in want:
+                            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (i, axis, side, off, q, k)
+                        mirror_camera(s, o)
+                        orc_check(oracle, o, fast, spp, row0=row_step - 1, row_step=row_step, compact=True, use_bvh=0,
+                                  ctx=(i, axis, side, off, q))
+                        n += 1
+                        skies += int((full["hit_inst"] < 0).all())
+    assert n > 50 and skies < n
+
+
 @pytest.mark.parametrize("col1", [(0.9, 0.8, 0.7, 1.0), (0.9, -0.0, 0.7, 1.0)])
 def test_unlit_skip_exact(gpu, oracle, col1):
     """The fast kernels trace no shadow segments for a light whose phong factor (diffuse +
