@@ -1772,9 +1772,15 @@ __device__ __forceinline__ bool grown_box_maybe(float4 lo, float4 hi, float A, f
     return !(tl > th);
 }
 
-__device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const SceneView& S, int g) {
+// The group's ray cone (cone_misses_root): its four corner directions, the side planes'
+// normals (pointing inward), the largest direction component; ok = 0 when no direction
+// component comes near zero over the rectangle is not guaranteed (then nothing is decided).
+struct GroupCone { V3 k[4], n[4]; float dmax; int ok; };
+__device__ __forceinline__ GroupCone group_cone(const TraceParams& P, int g) {
+    GroupCone gc;
+    gc.ok = 0;
     const DCamera& c = P.cam;
-    if (!(c.near_ > 0.0f) || S.n_real < 2) return false;
+    if (!(c.near_ > 0.0f)) return gc;
     const int gy = (int)udiv((unsigned)g, P.div_ngx), gx = g - gy * P.n_gx;
     const int pr0 = gy * P.gh;
     const float e = 1.0f / 64.0f;
@@ -1785,42 +1791,80 @@ __device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const Sce
         const float a = (cx - 0.5f * c.W) / c.unit, b = (0.5f * c.H - cy) / c.unit;
         return (c.near_ * c.f + a * c.r) + b * c.u;
     };
-    const V3 k0 = D(x0, y0), k1 = D(x1, y0), k2 = D(x1, y1), k3 = D(x0, y1);
+    gc.k[0] = D(x0, y0); gc.k[1] = D(x1, y0); gc.k[2] = D(x1, y1); gc.k[3] = D(x0, y1);
     const V3 mid = D(0.5f * (x0 + x1), 0.5f * (y0 + y1));
     auto amax = [](V3 v) { return fmaxf(fabsf(v.x), fmaxf(fabsf(v.y), fabsf(v.z))); };
-    const float dmax = fmaxf(fmaxf(amax(k0), amax(k1)), fmaxf(amax(k2), amax(k3)));
-    const float tiny = 0x1p-40f * dmax;
+    gc.dmax = fmaxf(fmaxf(amax(gc.k[0]), amax(gc.k[1])), fmaxf(amax(gc.k[2]), amax(gc.k[3])));
+    const float tiny = 0x1p-40f * gc.dmax;
     auto near0 = [&](float a, float b, float cc, float d) {
         return fminf(fminf(a, b), fminf(cc, d)) <= tiny && fmaxf(fmaxf(a, b), fmaxf(cc, d)) >= -tiny;
     };
-    if (near0(k0.x, k1.x, k2.x, k3.x) || near0(k0.y, k1.y, k2.y, k3.y) || near0(k0.z, k1.z, k2.z, k3.z)) return false;
-    V3 n[4] = {cross(k0, k1), cross(k1, k2), cross(k2, k3), cross(k3, k0)};
+    const V3* k = gc.k;
+    if (near0(k[0].x, k[1].x, k[2].x, k[3].x) || near0(k[0].y, k[1].y, k[2].y, k[3].y) || near0(k[0].z, k[1].z, k[2].z, k[3].z))
+        return gc;
 #pragma unroll
-    for (int i = 0; i < 4; i++) if (dot(n[i], mid) < 0.0f) n[i] = neg(n[i]);
+    for (int i = 0; i < 4; i++) {
+        gc.n[i] = cross(k[i], k[(i + 1) & 3]);
+        if (dot(gc.n[i], mid) < 0.0f) gc.n[i] = neg(gc.n[i]);
+    }
+    gc.ok = 1;
+    return gc;
+}
+// Whether no ray of the cone meets box [mn, mx] (nd = 0: a degenerate box, never hit), with
+// conservative margins: the box grown by 1e-4 of its coordinate scale, separations beyond the
+// rays' rounding (1e-5 relative).
+__device__ __forceinline__ bool cone_outside(const GroupCone& gc, V3 pos, V3 mn, V3 mx, bool nd) {
+    if (!nd) return true;
+    auto amax = [](V3 v) { return fmaxf(fabsf(v.x), fmaxf(fabsf(v.y), fabsf(v.z))); };
+    const float m = 1e-4f * (fmaxf(amax(mn), amax(mx)) + amax(pos)) + 1e-30f;
+    mn = mn - v3(m, m, m); mx = mx + v3(m, m, m);
+    // a box face plane: the apex beyond it and every direction pointing away from it by
+    // more than the rounding of the computed rays (1e-5 relative)
+    const float away = 1e-5f * gc.dmax;
+    const V3* k = gc.k;
+    auto face = [&](float o, float lo, float hi, float a0, float a1, float a2, float a3) {
+        return (o > hi && fminf(fminf(a0, a1), fminf(a2, a3)) >= away) || (o < lo && fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) <= -away);
+    };
+    bool sep = face(pos.x, mn.x, mx.x, k[0].x, k[1].x, k[2].x, k[3].x) || face(pos.y, mn.y, mx.y, k[0].y, k[1].y, k[2].y, k[3].y) ||
+               face(pos.z, mn.z, mx.z, k[0].z, k[1].z, k[2].z, k[3].z);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const V3 nn = gc.n[i];
+        const V3 q = v3(nn.x >= 0.0f ? mx.x : mn.x, nn.y >= 0.0f ? mx.y : mn.y, nn.z >= 0.0f ? mx.z : mn.z) - pos;
+        const float sv = dot(nn, q);
+        const float tol = 1e-5f * (fabsf(nn.x) + fabsf(nn.y) + fabsf(nn.z)) * (fabsf(q.x) + fabsf(q.y) + fabsf(q.z));
+        sep = sep || sv < -tol;
+    }
+    return sep;
+}
+__device__ __forceinline__ bool cone_misses_root(const TraceParams& P, const SceneView& S, int g) {
+    if (S.n_real < 2) return false;
+    const GroupCone gc = group_cone(P, g);
+    if (!gc.ok) return false;
     const float4* rec = S.fnode;                               // the root's two children (pair_hit_at)
     const float4 A = rec[0], B = rec[1], C = rec[2];
-    auto outside = [&](V3 mn, V3 mx, bool nd) {
-        if (!nd) return true;                                  // degenerate: never hit
-        const float m = 1e-4f * (fmaxf(amax(mn), amax(mx)) + amax(c.pos)) + 1e-30f;
-        mn = mn - v3(m, m, m); mx = mx + v3(m, m, m);
-        // a box face plane: the apex beyond it and every direction pointing away from it by
-        // more than the rounding of the computed rays (1e-5 relative)
-        const float away = 1e-5f * dmax;
-        auto face = [&](float o, float lo, float hi, float a0, float a1, float a2, float a3) {
-            return (o > hi && fminf(fminf(a0, a1), fminf(a2, a3)) >= away) || (o < lo && fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)) <= -away);
-        };
-        bool sep = face(c.pos.x, mn.x, mx.x, k0.x, k1.x, k2.x, k3.x) || face(c.pos.y, mn.y, mx.y, k0.y, k1.y, k2.y, k3.y) ||
-                   face(c.pos.z, mn.z, mx.z, k0.z, k1.z, k2.z, k3.z);
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const V3 q = v3(n[i].x >= 0.0f ? mx.x : mn.x, n[i].y >= 0.0f ? mx.y : mn.y, n[i].z >= 0.0f ? mx.z : mn.z) - c.pos;
-            const float sv = dot(n[i], q);
-            const float tol = 1e-5f * (fabsf(n[i].x) + fabsf(n[i].y) + fabsf(n[i].z)) * (fabsf(q.x) + fabsf(q.y) + fabsf(q.z));
-            sep = sep || sv < -tol;
-        }
-        return sep;
-    };
-    return outside(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), A.x <= B.z) && outside(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), A.y <= B.w);
+    return cone_outside(gc, P.cam.pos, v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), A.x <= B.z) &&
+           cone_outside(gc, P.cam.pos, v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), A.y <= B.w);
+}
+// Brute-force frames (item 30): whether no ray of the cone comes within the grown slack of
+// any instance box.  A ray meets box k grown by A + B t only at times t <= (F + A) / (1 - B), F the
+// distance from the camera to the box's farthest corner, so growing the box by
+// G = A + B (F + A) / (1 - B), doubled for rounding, covers every such t.
+__device__ __forceinline__ bool cone_misses_boxes(const TraceParams& P, int g, const float4* lo, const float4* hi, int nb,
+                                                  float A, float B) {
+    const GroupCone gc = group_cone(P, g);
+    if (!gc.ok) return false;
+    const V3 pos = P.cam.pos;
+    for (int k = 0; k < nb; k++) {
+        const float4 l = lo[k], h = hi[k];
+        if (!(l.x <= h.x)) continue;                           // an empty mesh: never hit
+        const V3 far = v3(fmaxf(fabsf(l.x - pos.x), fabsf(h.x - pos.x)), fmaxf(fabsf(l.y - pos.y), fabsf(h.y - pos.y)),
+                          fmaxf(fabsf(l.z - pos.z), fabsf(h.z - pos.z)));
+        const float F = (far.x + far.y) + far.z;               // >= the farthest corner's distance
+        const float G = 2.0f * (A + B * (F + A) / (1.0f - B));
+        if (!cone_outside(gc, pos, v3(l.x - G, l.y - G, l.z - G), v3(h.x + G, h.y + G, h.z + G), true)) return false;
+    }
+    return true;
 }
 
 // One block of 4 waves per 64 consecutive groups: wave 0 runs the cone test, one group per
@@ -1875,7 +1919,8 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     if (wv == 0) {
         const int gl = base + lane;
         const bool in = lane < n_in;
-        const bool csky = in && !brute && cone_misses_root(P, S, gl);
+        const bool csky = in && (brute ? cone_misses_boxes(P, gl, s_blo, s_bhi, nb, 2.0f * P.sky_A, P.sky_B)
+                                       : cone_misses_root(P, S, gl));
         // Representative ray: a group the cone test leaves undecided is live as
         // soon as one of its primaries enters the root -- lane 0's (pixel 0, sample 0), the
         // trace kernel's own ray and test -- so only the groups whose representative misses

@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
 O=gpurun_out/r05/bsky; mkdir -p $O
-timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_render.py -k "brute or frame_parity or update_scene" tests/test_gpu_fullsize.py::test_world1_1080p_brute_force > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 400 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_render.py -k "brute or frame_parity or update_scene or sky_prepass or spp8_sky" tests/test_gpu_fullsize.py::test_world1_1080p_brute_force > $O/pytest.log 2>&1 || { echo "tests failed"; tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for i in 1 2 3; do
   for v in on off; do
