@@ -1877,7 +1877,8 @@ __device__ __forceinline__ bool cone_misses_boxes(const TraceParams& P, int g, c
 #define RT_SKY_WAVES 4       // waves per sky_kernel block (64 groups per block)
 #endif
 constexpr int SKY_THREADS = 64 * RT_SKY_WAVES;
-static_assert(SKY_THREADS >= 128, "sky_kernel's heavy-list append uses threads 64..127");
+// the heavy-list append runs on threads 64..127 beside the live list's 0..63 (one wave: after it)
+constexpr int SKY_HOFF = SKY_THREADS >= 128 ? 64 : 0;
 template <bool BRUTE>
 __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneView S, unsigned char* gsky, int* live) {
     __shared__ unsigned long long s_sky, s_todo;
@@ -2012,11 +2013,11 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     const int q = blockIdx.x % NQ, n = s_cnt, nh = s_hcnt;
     if (n == 0 && nh == 0) return;
     if (threadIdx.x == 0 && n) s_base = atomicAdd(&P.work[16 * (NQ + 1 + q)], n);
-    if (threadIdx.x == 64 && nh) s_hbase = atomicAdd(&P.work[WORK_HEAVY_LEN], nh);
+    if ((int)threadIdx.x == SKY_HOFF + (SKY_HOFF ? 0 : 1) && nh) s_hbase = atomicAdd(&P.work[WORK_HEAVY_LEN], nh);
     __syncthreads();
     if ((int)threadIdx.x < n) live[q * P.live_cap + s_base + threadIdx.x] = s_list[threadIdx.x];
-    if ((int)threadIdx.x >= 64 && (int)threadIdx.x < 64 + nh)            // heavy list after the NQ lists
-        live[NQ * P.live_cap + s_hbase + threadIdx.x - 64] = s_hlist[threadIdx.x - 64];
+    if ((int)threadIdx.x >= SKY_HOFF && (int)threadIdx.x < SKY_HOFF + nh)   // heavy list after the NQ lists
+        live[NQ * P.live_cap + s_hbase + threadIdx.x - SKY_HOFF] = s_hlist[threadIdx.x - SKY_HOFF];
 }
 
 // ---------------------------------------------------------------------------
