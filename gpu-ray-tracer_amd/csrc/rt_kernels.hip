@@ -222,6 +222,9 @@ struct BvhRefs {
 #ifndef RT_HEAVY_STATIC
 #define RT_HEAVY_STATIC 1    // frames issued alone: heavy-list tickets assigned statically (trace_kernel)
 #endif
+#ifndef RT_TPC_WIDE
+#define RT_TPC_WIDE 16       // live-list tickets of one-pixel groups (spp >= 64, M_PART): 16 consecutive pixels
+#endif
 #ifndef RT_LDS_SUM
 #define RT_LDS_SUM 1         // spp >= 16 in parked kernels: per-channel in-order sample sums through LDS
 #endif
@@ -1468,6 +1471,17 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         inflight = 1;
     };
     auto resolve = [&]() { inflight = 0; return __builtin_amdgcn_readfirstlane(pend); };   // all lanes active here
+    // one-pixel groups (LSUM kernels, spp >= 64): RGBA results of consecutive pixels buffered one
+    // per lane (wbuf), stored as one piece when the run breaks: a 4-B store per pixel-wave left
+    // as its own memory-side write (config 5 wrote 20x its frame)
+    unsigned wbuf = 0;
+    int wbase = 0, wn = 0;                                     // (uniform) first pixel, count
+    auto wflush = [&]() {
+        if (wn > 0) {
+            if (lane_id_fresh() < wn) kparams().rgba[wbase + lane_id_fresh()] = wbuf;
+            wn = 0;
+        }
+    };
     request(qi);
     int tbase = resolve(), j = 0;
     const unsigned long long c_start = CYC ? __builtin_amdgcn_s_memtime() : 0;
@@ -1499,7 +1513,18 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
         auto umod = [&](unsigned n) { return n - udiv(n, kld(P.div_perq)) * (unsigned)per_q; };
         auto live_g = [&]() {
             const int n = live_n(qi);
-            const int i = (int)(((unsigned)ticket * 0x9E3779B1u) & (unsigned)(live_span(qi) - 1));
+            int i;
+            if (LSUM && kparams().tpc > 1) {
+                // a ticket's tpc (a power of two) consecutive indices stay consecutive list entries
+                // -- neighbouring pixels of one sky block -- and the runs are scrambled, so that a
+                // wave stores their results as one wide piece (wstore below)
+                const int rl = 31 - __builtin_clz((unsigned)kparams().tpc), span = live_span(qi);
+                if (span <= (1 << rl)) i = ticket;
+                else i = (int)((((((unsigned)ticket >> rl) * 0x9E3779B1u) & (unsigned)((span >> rl) - 1)) << rl) |
+                               ((unsigned)ticket & ((1u << rl) - 1u)));
+            } else {
+                i = (int)(((unsigned)ticket * 0x9E3779B1u) & (unsigned)(live_span(qi) - 1));
+            }
             return i < n ? ldc(P.live, ((q0 + qi) % NQ) * P.live_cap + i) : P.n_groups;
         };
         auto heavy_g = [&]() {                                 // hist = 2: the heavy live list, scrambled
@@ -1641,6 +1666,9 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             __builtin_amdgcn_wave_barrier();
         }
         const GroupLane go = group_lane(g);                    // the output pixel, recomputed here
+        const bool wide = LSUM && L == 64 && kparams().rgba != nullptr;   // (uniform) buffered RGBA stores
+        uint32_t w_enc = 0;
+        int w_pix = -1;
         if (go.valid && go.sub == 0) {
             KTP& P = kparams();
             const int p = go.pix;
@@ -1652,8 +1680,19 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             // Color(float r, g, b, a) truncation to uint8 and to_encoding (color.h:41-42, color.cu:23-26)
             const uint32_t enc = ((uint32_t)(uint8_t)((float)255 * mr) << 24) + ((uint32_t)(uint8_t)((float)255 * mg) << 16) +
                                  ((uint32_t)(uint8_t)((float)255 * mb) << 8) + (uint32_t)(uint8_t)((float)255 * ma);
-            if (P.rgba) P.rgba[p] = enc;
+            if (wide) { w_enc = enc; w_pix = p; }
+            else if (P.rgba) P.rgba[p] = enc;
             if (P.radiance) P.radiance[p] = make_float4(mean(sum_r.x), mean(sum_r.y), mean(sum_r.z), mean(sum_r.w));
+        }
+        if (wide) {                                            // lane 0 is the pixel's leader (L = 64)
+            const int pu = __builtin_amdgcn_readlane(w_pix, 0);
+            const unsigned eu = (unsigned)__builtin_amdgcn_readlane((int)w_enc, 0);
+            if (pu >= 0) {
+                if (wn > 0 && (pu != wbase + wn || wn == 64)) wflush();
+                if (wn == 0) wbase = pu;
+                asm("v_writelane_b32 %0, %1, m0" : "+v"(wbuf) : "s"(eu), "{m0}"(wn));
+                wn++;
+            }
         }
         if (STATS && P.stats && lane == 0) {                 // profiling: heaviest group (PROF: rt_profile_groups)
             atomicMax(&P.stats[20], __builtin_amdgcn_s_memrealtime() - g_t0);
@@ -1691,6 +1730,7 @@ __global__ __launch_bounds__(TRACE_BLOCK_P) void trace_kernel(TraceParams P_arg,
             }
         }
     }
+    if (LSUM) wflush();
     if (P.hist == 1 && lane == 0 && wave_sum) atomicAdd(&P.hctl_next[1], wave_sum);
     if (CYC && P.stats && lane == 0) {
         if (wc.rays) atomicAdd(&P.stats[0], wc.rays);
@@ -3208,7 +3248,7 @@ int launch_trace(rt_scene* s, const rt_render_opts& o, hipStream_t st, uint32_t*
         P.gsky = s->d_gsky;
         P.live = s->d_live; P.live_cap = lcap;
         if (s->n_slots > 1 && grew) { int r; if ((r = mirror_slot_caps(s)) != RT_OK) return r; }
-        P.tpc = RT_TPC_LIVE;
+        P.tpc = (part_k && P.lanes_per_px == 64) ? RT_TPC_WIDE : RT_TPC_LIVE;
         const Box* mbox = s->d_mesh_box;
         float sky_A = S.prune_abs, sky_B = 0x1p-12f;          // brute-force frames: the grown boxes' slack
         void* sargs[] = {&P, &S, &s->d_gsky, &s->d_live, &mbox, &sky_A, &sky_B};

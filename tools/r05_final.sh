@@ -6,7 +6,8 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$R" || exit 1
-O=gpurun_out/r05/final
+F=${FINAL:-r05/final}
+O=gpurun_out/$F
 mkdir -p $O
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
@@ -16,10 +17,10 @@ timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 > $O/bench20_1.log 2
 timeout -k 10 200 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20_2.log 2>&1 || { echo "bench 2 failed"; exit 1; }
 timeout -k 10 200 python3 -u bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-camera-path > $O/bench60.log 2>&1 || { echo "bench60 failed"; exit 1; }
 for f in bench20_1 bench20_2 bench60; do tail -1 $O/$f.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(sys.argv[1], d['ms_per_step'], d['value'], d.get('frame_latency_ms'), (d.get('camera_path') or {}).get('ms_per_step'))" $f; done
-timeout -k 10 600 bash tools/profile_step.sh r05/final/step_w8s > $O/profile_step.log 2>&1 || { echo "profile_step failed"; tail $O/profile_step.log; exit 1; }
+timeout -k 10 600 bash tools/profile_step.sh $F/step_w8s > $O/profile_step.log 2>&1 || { echo "profile_step failed"; tail $O/profile_step.log; exit 1; }
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/kt20" -o kt20 -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-camera-path > "$R/$O/kt20.log" 2>&1) || { echo "kt20 failed"; exit 1; }
-timeout -k 10 900 bash tools/profile.sh r05/final/prof_w8s > $O/profile.log 2>&1 || { echo "profile failed"; tail $O/profile.log; exit 1; }
-QUICK=1 timeout -k 10 400 bash tools/profile.sh r05/final/prof_w16 --scene world16 --width 3840 --height 2160 --spp 64 > $O/prof_w16.log 2>&1 || { echo "profile w16 failed"; tail $O/prof_w16.log; exit 1; }
+timeout -k 10 900 bash tools/profile.sh $F/prof_w8s > $O/profile.log 2>&1 || { echo "profile failed"; tail $O/profile.log; exit 1; }
+QUICK=1 timeout -k 10 400 bash tools/profile.sh $F/prof_w16 --scene world16 --width 3840 --height 2160 --spp 64 > $O/prof_w16.log 2>&1 || { echo "profile w16 failed"; tail $O/prof_w16.log; exit 1; }
 W16="--scene world16 --width 3840 --height 2160 --spp 64 --steps 6 --warmup 2 --no-cpu-baseline --no-camera-path"
 timeout -k 10 300 python3 -u bench.py $W16 > $O/cfg_world16.log 2>&1 || { echo "w16 failed"; exit 1; }
 timeout -k 10 300 python3 -u bench.py $W16 --scene world16_tex --textures > $O/cfg_world16_tex.log 2>&1 || { echo "w16tex failed"; exit 1; }
