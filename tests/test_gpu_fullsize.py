@@ -161,3 +161,24 @@ def test_config5_full_size(gpu, oracle, scene, textures):
     st = counted["stats"]
     assert (st["rays"], st["nodes"], st["leaves"], st["tri_tests"]) == tuple(int(x) for x in of["stats"])
     assert (fast["hit_inst"] >= 0).mean() > 0.2
+
+
+@pytest.mark.parametrize("w,h", [(203, 45), (37, 29)])
+def test_config5_wide_store_runs(gpu, oracle, w, h):
+    """Config 5's one-pixel groups store RGBA 16 consecutive pixels at a time (DESIGN §3.2 item 31:
+    live tickets in runs of 16, a run flushed when the next pixel is not adjacent, after 64
+    pixels, or when the wave leaves its loop).  Widths that are no multiple of 16, row ends inside
+    a run, and compact row slices (each slice row ends a run) against the oracle, RGBA only (the
+    wide path) and with every output; pipelined as bench.py issues frames."""
+    spp = 64
+    s = gpu.Scene.load_json(scene_path("world16"), w, h)
+    of = oracle.render(oracle.load(scene_path("world16"), w, h), spp=spp, nthreads=NTHREADS)
+    only = s.render(spp=spp, want=("rgba",), stats=False)
+    assert np.array_equal(only["rgba"], of["rgba"]), int((only["rgba"] != of["rgba"]).sum())
+    fast = s.render(spp=spp, want=WANT, stats=False)
+    assert_frames_equal(fast, of, ctx="world16 %dx%d" % (w, h))
+    for row0, step in [(1, 3), (0, 2)]:
+        sl = s.render(spp=spp, row0=row0, row_step=step, compact=True, want=("rgba",), stats=False)
+        assert np.array_equal(sl["rgba"], of["rgba"][row0::step]), (row0, step)
+    piped = _pipelined(gpu, "world16", spp, world=3, rank=1, n_frames=10, size=(w, h))
+    assert np.array_equal(piped, of["rgba"][1::3])
