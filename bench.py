@@ -83,18 +83,33 @@ def parse():
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
     p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
-    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "stream-last-full"),
+    p.add_argument("--grid", default=os.environ.get("RT_BENCH_GRID", "stream"),
                    choices=("stream", "half", "full", "last-full", "stream-last-full"),
-                   help="grid of the timed frames (rt_scene_set_overlap): stream-last-full (default) = stream, "
-                        "with the timed region's last frame on every CU (no frame follows it: -3%% at 20 steps, "
-                        "DESIGN.md 4.1); stream = half the CUs for every frame, "
-                        "the first included (RT_OVERLAP_STREAM); half = half the CUs for a frame issued while "
+                   help="grid of the timed frames (rt_scene_set_overlap): stream (default: the steady state a "
+                        "caller that always has another frame behind sees) = half the CUs for every frame, "
+                        "the first included (RT_OVERLAP_STREAM); stream-last-full = stream, with the timed "
+                        "region's last frame on every CU (no frame follows it; DESIGN.md 4.1); "
+                        "half = half the CUs for a frame issued while "
                         "another runs; full = every CU; last-full = half except the timed region's last frame; "
                         "stream-last-full = stream except the timed region's last frame (every CU)")
+    p.add_argument("--no-device-resident", action="store_true",
+                   help="skip the device-resident figure (the same K frames left in HBM)")
+    p.add_argument("--frame-crcs", action="store_true",
+                   help="rank 0 reports the CRC-32 of every timed host frame (tests: each frame the pipeline "
+                        "assembles, not only the last)")
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="nccl = RCCL over xGMI (the driver's runs); gloo stages the gather through host "
                         "memory and lets several ranks share one GPU (testing the N > 1 path on one GPU)")
     return p.parse_args()
+
+
+def lib_sha16():
+    """The product library this run loaded (profiles/pmc_step.json entries record it too)."""
+    import hashlib
+    try:
+        return hashlib.sha256(open(rtamd.LIB_PATH, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 def cgroup_cpu_quota():
@@ -235,98 +250,200 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     rtamd.set_device(dev)
+    depth = max(1, min(8, args.frames_in_flight))
+    overlap = not args.no_overlap and depth > 1
+    H0, W0 = args.height, args.width
+    if overlap:
+        # frames in flight (rtamd.dist.FramePipeline).  `fbr` copies every finished frame to pinned
+        # host memory on a copy engine (the reference's post-condition: the headline); `fb` leaves
+        # frames in HBM (the device-resident figure).  Both share the render streams, created and
+        # first used here, before the scene exists: a torch stream's HIP stream is created at its
+        # first use (1-7 ms each, profiles/r06/cold/), the caller's one-time cost, not a frame's.
+        fbr = rtdist.FramePipeline(W0, H0, world, rank, "cuda", dist, depth=depth, readback=True, host_staging=gloo)
+        fb = rtdist.FramePipeline(W0, H0, world, rank, "cuda", dist, depth=depth, streams=fbr.streams,
+                                  host_staging=gloo)
+        for st_ in fbr.streams + ([fbr.copy_stream] if getattr(fbr, "copy_stream", None) is not None else []):
+            torch.cuda.Event().record(st_)
+        torch.cuda.synchronize()
     scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")
+    # procedural::gpu::generate: the scene goes to the device and one untimed frame warms it
+    # (rt_scene_load_json with a gfx950 device present, include/rt_amd.h)
+    t_load = time.perf_counter()
     scene = rtamd.Scene.load_json(scene_path, args.width, args.height)
     if args.textures:
         scene.load_atlas()
+    if overlap:
+        scene.set_frame_slots(depth)
+    torch.cuda.synchronize()
+    load_ms = (time.perf_counter() - t_load) * 1e3
     W, H = scene.width, scene.height
+    assert (W, H) == (W0, H0), (W, H, W0, H0)
     my_rows = len(rtdist.rows_of(rank, world, H))
     stream = torch.cuda.current_stream()
     use_bvh = not args.brute
     frame_no = [0]
-    depth = max(1, min(8, args.frames_in_flight))
-    overlap = not args.no_overlap and not gloo and depth > 1
-    if overlap:                           # frames in flight (rtamd.dist.FramePipeline)
-        scene.set_frame_slots(depth)
-        fb = rtdist.FramePipeline(W, H, world, rank, "cuda", dist, depth=depth)
-        part = fb.parts[0]
-    else:                                 # serial frames; RCCL gather of frame k overlaps frame k+1
+    if not overlap:                       # serial frames; RCCL gather of frame k overlaps frame k+1
         fb = rtdist.RowCyclicFrame(W, H, world, rank, "cuda", dist, host_staging=gloo, slots=2)
-        part = fb.part
+        fbr = None
+    part = fb.parts[0]
 
     def render(buf, st, timing):
         scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
                             compact=True, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream,
                             timing=timing, textures=args.textures)
 
-    def step(timing):
+    def step(timing, pipe=None):
+        """Issue one frame (device-resident pipeline unless `pipe` is given)."""
         k = frame_no[0]
         frame_no[0] += 1
         if overlap:
-            fb.step(k, lambda buf, st: render(buf, st, timing))
+            (pipe or fb).step(k, lambda buf, st: render(buf, st, timing))
         else:
             render(fb.slot_part(k), stream, timing)
             fb.gather(k)
+        return k
 
+    def host_step(timing=False):
+        """Issue one host-readable frame; returns its number."""
+        if overlap:
+            return step(timing, fbr)
+        return step(timing)
+
+    def host_read(k):
+        """Rank 0: frame k on the host (waits for its copy-engine transfer)."""
+        if overlap:
+            return fbr.host_frame(k)
+        fb.finish()
+        return fb.frame.cpu()
+
+    def set_grid(last=False):
+        if not overlap:
+            return
+        if args.grid == "full" or (last and args.grid in ("last-full", "stream-last-full")):
+            scene.set_overlap(True)                         # nothing is issued behind the last frame
+        elif args.grid in ("stream", "stream-last-full"):
+            scene.set_overlap(False, stream=True)           # the timed frames are issued back to back
+        else:
+            scene.set_overlap(False)
+
+    crcs = {}
+
+    def consume(k, lag, first=0):
+        """Rank 0's host consumer: reads frame k - lag (from `first` on: the frames issued through
+        the host-readable pipeline), in order (the reference's caller blits the canvas after every
+        update_scene, main.cc:180-196)."""
+        j = k - lag
+        if rank == 0 and j >= first and (overlap or lag == 0):
+            h = host_read(j)
+            if args.frame_crcs:
+                import zlib
+                crcs[j] = zlib.crc32(h.numpy().tobytes())
+
+    lag = (fbr.n_host - 1) if overlap else 0
+
+    def host_frames(n, moving=False, last_full=True):
+        """n host-readable frames issued back to back, each read by the host consumer; returns the
+        first and last frame numbers.  The caller brackets the timing."""
+        set_grid()
+        first = None
+        for i in range(n):
+            if moving:
+                camera_move(scene)
+            if last_full and i == n - 1:
+                set_grid(last=True)
+            k = host_step()
+            first = k if first is None else first
+            consume(k, lag, first)
+        if overlap:
+            fbr.finish()
+        if rank == 0:
+            for j in range(max(first, k - lag + 1) if overlap else k + 1, k + 1):   # the frames still unread
+                consume(j, 0)
+        torch.cuda.synchronize()
+        if overlap:
+            scene.set_overlap(False)
+        return first, k
+
+    # The reference's own benchmark (main.cc:210-216): the first frame after the scene is made,
+    # host-readable (here: the first host-readable frame after load, at this run's spp and size).
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    tc = time.perf_counter()
+    k0 = host_step()
+    if overlap:
+        fbr.finish()
+    if rank == 0:
+        host_read(k0)
+    torch.cuda.synchronize()
+    cold_ms = (time.perf_counter() - tc) * 1e3
     # per-frame work counters (deterministic): one untimed counted render of this rank's rows
     st = scene.render_device(spp=args.spp, use_bvh=use_bvh, rebuild_bvh=True, row0=rank, row_step=world,
                              compact=True, rgba_ptr=part.data_ptr(), stream=stream.cuda_stream, sync=True, stats=True,
                              textures=args.textures)
-    # first fast frame: no scheduling history yet (longest-first needs one measured frame)
-    torch.cuda.synchronize()
-    tc = time.perf_counter()
-    step(False)
-    fb.finish()
-    torch.cuda.synchronize()
-    cold_ms = (time.perf_counter() - tc) * 1e3
-    for _ in range(max(0, args.warmup - 1)):
-        step(False)
+    if args.warmup > 1:
+        host_frames(args.warmup - 1)
     scene.timing_collect()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    if overlap and args.grid == "full":
-        scene.set_overlap(True)
-    if overlap and args.grid in ("stream", "stream-last-full"):
-        scene.set_overlap(False, stream=True)               # the timed frames are issued back to back
+
+    # ---- the headline: K host-readable frames (SURVEY §8d: to the framebuffer on the host,
+    # gathered to rank 0 for N > 1) ----
+    crcs.clear()
     rtamd.profile_marker(1, stream.cuda_stream)             # the timed window starts (tools/pmc_step.py)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        if overlap and args.grid in ("last-full", "stream-last-full") and i == args.steps - 1:
-            scene.set_overlap(True)                         # nothing is issued behind the last frame
-        step(not args.no_kernel_timing and not overlap)
-    fb.finish()                                             # the last frame's gather + un-permute
-    torch.cuda.synchronize()
+    f_first, f_last = host_frames(args.steps, last_full=True)
     if dist:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     rtamd.profile_marker(2, stream.cuda_stream)             # ... and ends
+    timed_crcs = [crcs.get(j) for j in range(f_first, f_last + 1)]
     if args.dump_frame and rank == 0:
         import numpy as np
-        np.save(args.dump_frame, fb.frame.cpu().numpy().view(np.uint32))
-    if overlap:
-        scene.set_overlap(False)
+        np.save(args.dump_frame, host_read(f_last).numpy().view(np.uint32) if overlap else fb.frame.cpu().numpy().view(np.uint32))
+
+    # ---- the same frames left in HBM (no host copy): the device-resident figure ----
+    dev_s = None
+    if not args.no_device_resident:
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        set_grid()
+        t2 = time.perf_counter()
+        for i in range(args.steps):
+            if i == args.steps - 1:
+                set_grid(last=True)
+            step(False)
+        fb.finish()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        dev_s = time.perf_counter() - t2
+        if overlap:
+            scene.set_overlap(False)
     tm = scene.timing_collect()
-    # latency of one frame issued alone (render + gather + un-permute, waited for); with frames
-    # in flight the kernels' event-timed durations come from these lone frames (a launch that
-    # overlaps other frames' kernels is longer than its cost)
+    # latency of one host-readable frame issued alone (render + gather + un-permute + copy to the
+    # host, waited for); with frames in flight the kernels' event-timed durations come from these
+    # lone frames (a launch that overlaps other frames' kernels runs longer than its cost)
     lat = []
     for _ in range(max(3, args.steps // 2)):
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t3 = time.perf_counter()
-        step(overlap and not args.no_kernel_timing)
-        fb.finish()
+        k = host_step(not args.no_kernel_timing)
+        if overlap:
+            fbr.finish()
+        if rank == 0:
+            host_read(k)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t3)
     lat_ms = sorted(lat)[len(lat) // 2] * 1e3
-    if overlap:
-        tm = scene.timing_collect()
+    tm = scene.timing_collect()
     # Moving camera (the reference's real caller moves it every frame, main.cc:140-180): the
-    # same K timed frames with main.cc's key and mouse steps applied before each, so the
+    # same K host-readable frames with main.cc's key and mouse steps applied before each, so the
     # previous frame's heavy-group flags (history-driven scheduling) are one pose stale.
     # Rays in the reference's units from a counted replay of the same poses (untimed).
     cam_path = None
@@ -335,23 +452,11 @@ def main():
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
-        if overlap and args.grid == "full":
-            scene.set_overlap(True)
-        if overlap and args.grid in ("stream", "stream-last-full"):
-            scene.set_overlap(False, stream=True)
         tc0 = time.perf_counter()
-        for i in range(args.steps):
-            camera_move(scene)
-            if overlap and args.grid in ("last-full", "stream-last-full") and i == args.steps - 1:
-                scene.set_overlap(True)                     # as in the headline's timed loop
-            step(False)
-        fb.finish()
-        torch.cuda.synchronize()
+        host_frames(args.steps, moving=True)
         if dist:
             dist.barrier()
         cam_s = time.perf_counter() - tc0
-        if overlap:
-            scene.set_overlap(False)
         scene.set_camera(pos0, quat0)
         cam_rays = 0
         for i in range(args.steps):
@@ -362,48 +467,6 @@ def main():
             cam_rays += int(cst["rays"])
         scene.set_camera(pos0, quat0)
         cam_path = (cam_s, cam_rays)
-    # host-readable frames (the reference's post-condition, raytracer.cu:102-120): the same
-    # pipeline with an asynchronous copy of every finished frame into pinned host memory;
-    # the timed region ends when the last frame is on the host (serial frames: a blocking
-    # copy per frame).  Per-rank max like the headline.
-    n_rb = max(4, args.steps)
-    if overlap:
-        # a consumer of every frame on the host: frames issued while others run keep every CU
-        # (rt_scene_set_overlap; with half the CUs the copies measured 12% slower)
-        scene.set_overlap(True)
-        fbr = rtdist.FramePipeline(W, H, world, rank, "cuda", dist, depth=depth, readback=True)
-        for k in range(depth + 1):                          # warm the host buffers and streams
-            fbr.step(k, lambda buf, st: render(buf, st, False))
-        fbr.finish()
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        t2 = time.perf_counter()
-        for k in range(n_rb):
-            f = depth + 1 + k
-            fbr.step(f, lambda buf, st: render(buf, st, False))
-            if rank == 0 and f - fbr.n_host + 1 >= 0:
-                fbr.host_frame(f - fbr.n_host + 1)          # a host consumer reads every frame, in order,
-                #                                             host_buffers - 1 (= 2 x depth - 1) behind
-        fbr.finish()
-        if rank == 0:
-            fbr.host_frame(depth + n_rb)                    # the last frame is host-readable
-        torch.cuda.synchronize()
-        rb_s = time.perf_counter() - t2
-        scene.set_overlap(False)
-    else:
-        t2 = time.perf_counter()
-        for _ in range(n_rb):
-            step(False)
-            fb.finish()
-            if rank == 0:
-                fb.frame.cpu()
-        torch.cuda.synchronize()
-        rb_s = time.perf_counter() - t2
-    rb_t = torch.tensor([rb_s], dtype=torch.float64, device="cpu" if gloo else "cuda")
-    if dist:
-        dist.all_reduce(rb_t, op=dist.ReduceOp.MAX)
-    rb_ms = float(rb_t.item()) / n_rb * 1e3
     # what the fast kernels actually do for this rank's rows (profiling run, untimed)
     try:
         work = scene.frame_work(spp=args.spp, row0=rank, row_step=world, compact=True) \
@@ -415,12 +478,12 @@ def main():
     local_rays = torch.tensor([st["rays"], st["nodes"], st["leaves"], st["tri_tests"],
                                work["queries"] if work else 0, work["leaf_lanes"] if work else 0],
                               dtype=torch.float64, device=red_dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor([elapsed, dev_s if dev_s is not None else 0.0], dtype=torch.float64, device=red_dev)
     if dist:
         dist.all_reduce(local_rays, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     rays, nodes, leaves, tris, queries, leaf_lanes = [float(x) for x in local_rays.cpu()]
-    elapsed = float(tmax.item())
+    elapsed, dev_s = float(tmax[0].item()), (float(tmax[1].item()) if dev_s is not None else None)
     if cam_path:
         cp = torch.tensor([cam_path[0], float(cam_path[1])], dtype=torch.float64, device=red_dev)
         cps = cp[1:].clone()
@@ -458,6 +521,7 @@ def main():
     algo_bytes = frame_bytes + (work["scene_bytes"] if work else 0)
     ref_bytes = B_NODE * nodes / world + B_LEAF * leaves / world + frame_bytes   # this rank's share
     roof = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": traffic,
+            "binding": None,
             "algorithmic_bytes_per_launch": int(algo_bytes),
             "algorithmic_GBs": round(algo_bytes / (trace_ms * 1e-3) / 1e9, 3),
             "launch_ms": round(trace_ms, 4)}
@@ -472,11 +536,12 @@ def main():
         achieved = algo_bytes / (trace_ms * 1e-3) / 1e9
         roof.update(achieved=round(achieved, 3), frac=round(achieved / HBM_PEAK_GBS, 5),
                     source="achieved = algorithmic bytes / event-timed launch (no PMC profile for this config)")
+    ref_gbs = ref_bytes / (trace_ms * 1e-3) / 1e9
     roof["reference_equivalent"] = {
-        "bytes_per_launch": int(ref_bytes), "GBs": round(ref_bytes / (trace_ms * 1e-3) / 1e9, 1),
+        "bytes_per_launch": int(ref_bytes), "GBs": round(ref_gbs, 1), "frac": round(ref_gbs / HBM_PEAK_GBS, 2),
         "note": "SURVEY 8d uncached model in the reference's units (28 B per BVH node test + 816 B per leaf, "
-                "counts of the reference traversal) -- not HBM traffic: the scene is LDS/L2-resident and the "
-                "fast kernel proves most of it unnecessary"}
+                "counts of the reference traversal) -- not HBM traffic: frac exceeds 1, so the kernel cannot be "
+                "doing this work from HBM; LDS residency of the tree and scene and the exact pruning serve it"}
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "strong",
@@ -491,14 +556,27 @@ def main():
                    # so that four render streams + main + collective + copy each get a queue)
                    "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]), "frames_in_flight": depth if overlap else 1,
                    "grid_timed_frames": args.grid if overlap else "full"},
+        "build": {"lib_sha16": lib_sha16()},
         "rays_unit": "reference-equivalent rays: every cast_ray of the reference's propagate_ray (SURVEY 8d), "
                      "counted by the counted kernel on the same frame",
-        "frame_ms": round(ms_per_step, 4), "ms_per_step_with_readback": round(rb_ms, 4),
-        "cold_frame_ms": round(cold_ms, 4), "frame_latency_ms": round(lat_ms, 4), "frames_in_flight": depth if overlap else 1,
+        "frame_ms": round(ms_per_step, 4),
+        "timed_to": "host-readable frames: every timed frame (rank 0: gathered and un-permuted) copied to pinned "
+                    "host memory by a copy engine and read by a host consumer; the window ends when the last "
+                    "frame is on the host (the reference's update_scene post-condition, raytracer.cu:102-120)",
+        "cold_frame_ms": round(cold_ms, 4), "scene_load_ms": round(load_ms, 3),
+        "cold_frame_note": "the first host-readable frame after scene load (main.cc:210-216's bench: the first "
+                           "update_scene after generate); scene_load_ms = load + upload + one untimed warm frame",
+        "frame_latency_ms": round(lat_ms, 4), "frames_in_flight": depth if overlap else 1,
         "rays_per_frame": int(rays), "nodes_per_frame": int(nodes), "leaves_per_frame": int(leaves),
         "tri_tests_per_frame": int(tris), "trace_kernel_ms": round(trace_ms, 4), "bvh_build_ms": round(bvh_ms, 4),
         "roofline": roof,
     }
+    if dev_s is not None:
+        out["device_resident"] = {
+            "ms_per_step": round(dev_s / args.steps * 1e3, 4), "value": round(rays * args.steps / dev_s / 1e6, 3),
+            "unit": "Mrays/s", "note": "the same K frames left in HBM (no host copy), measured after the headline"}
+    if args.frame_crcs and rank == 0:
+        out["frame_crcs"] = timed_crcs
     if work:
         out["queries_traced_per_frame"] = int(queries)
         out["queries_traced_Mrays_s"] = round(queries * args.steps / elapsed / 1e6, 3)
@@ -561,6 +639,31 @@ def main():
                                      ("issue_stalled", "SQ_WAIT_INST_ANY")) if c in ps}
         d["source"] = "SQ counters summed over the timed window's dispatches / steps (profiles/pmc_step.json)"
         out["issue_bound"]["per_step"] = d
+    if pst:
+        # the profiled window must be this run's kind of window: grid policy, frames in
+        # flight, what the timed region ends on, and the library build
+        want = {"grid_timed_frames": out["config"]["grid_timed_frames"], "frames_in_flight": out["frames_in_flight"],
+                "timed_to": "host" if overlap else "serial", "lib_sha16": lib_sha16()}
+        have = pst.get("window", {})
+        stale = sorted(k for k, v in want.items() if have.get(k) != v)
+        for blk in (roof.get("per_step"), out.get("issue_bound", {}).get("per_step")):
+            if blk is not None:
+                blk["matches_this_run"] = not stale
+                if stale:
+                    blk["differs_in"] = {k: [have.get(k), want[k]] for k in stale}
+    # What binds.  HBM is far below its roof (roofline.frac); the kernel is
+    # bound by VALU issue plus the traversal step's dependent latency, so the
+    # binding fraction is VALU wave-instructions issued over the CU array's issue peak.
+    if "issue_bound" in out:
+        ib = out["issue_bound"]
+        ps = ib.get("per_step")
+        src = ps if (ps and ps.get("matches_this_run", True)) else ib
+        roof["binding"] = {
+            "resource": "valu_issue", "frac": src["frac"], "achieved": src["achieved"], "peak": ib["peak"],
+            "unit": ib["unit"], "over": "the pipelined step (timed window's counters)" if src is ps else
+            "the lone trace launch", "lone_launch_frac": ib["frac"],
+            "note": "HBM frac above is the roofline the contract names; the kernel's binding resource is "
+                    "instruction issue (wave time: issuing / waiting on LDS and scalar loads / issue-stalled)"}
     if cam_path:
         out["camera_path"] = {
             "ms_per_step": round(cam_path[0] / args.steps * 1e3, 4), "steps": args.steps,

@@ -1966,7 +1966,11 @@ __global__ __launch_bounds__(SKY_THREADS) void sky_kernel(TraceParams P, SceneVi
     __shared__ unsigned long long s_sky, s_todo;
     __shared__ int s_cnt, s_base, s_list[64];
     __shared__ int s_hcnt, s_hbase, s_hlist[64];               // hist = 2: last frame's heavy groups
-    __shared__ float4 s_blo[64], s_bhi[64];                    // sky_brute: the instance boxes
+    // sky_brute: the instance boxes (2 KB); the tree's pass keeps its LDS footprint without them
+    struct Boxes { float4 lo[BRUTE ? 64 : 1], hi[BRUTE ? 64 : 1]; };
+    __shared__ Boxes s_bx;
+    float4* const s_blo = s_bx.lo;
+    float4* const s_bhi = s_bx.hi;
     const bool h2 = P.hist == 2;
     constexpr bool brute = BRUTE;
     int nb = 0;
@@ -3644,6 +3648,42 @@ int rt_spp_offset(int k, float* dx, float* dy) {
     return RT_OK;
 }
 
+int rt_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes <= 0) return fail(RT_ERR_ARG, "bytes > 0 and an output pointer required");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    HIPCHK(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    return RT_OK;
+}
+int rt_host_free(void* p) {
+    if (p) HIPCHK(hipHostFree(p));
+    return RT_OK;
+}
+// A device -> pinned-host copy on a DMA copy engine.  hipMemcpyDeviceToDeviceNoCU asks the
+// runtime for the SDMA path explicitly (the copy still goes where the pointers live: with a
+// hipHostMalloc destination it writes host memory over PCIe).  Measured on this image
+// (tools/copy_probe.hip, profiles/r06/copy/): 8.29 MB in 0.157 ms (53 GB/s), finished 0.66 ms
+// into a grid that held every CU for 3 ms, and no dispatch in the kernel trace; the torch
+// pinned-tensor copy the round-5 bench used ran as 320-us `__amd_rocclr_copyBuffer` blit kernels
+// that competed with the persistent trace blocks for CUs.
+int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, void* stream) {
+    if (!host_dst || !dev_src || bytes < 0) return fail(RT_ERR_ARG, "null pointer or negative size");
+    if (bytes == 0) return RT_OK;
+    HIPCHK(hipMemcpyAsync(host_dst, dev_src, (size_t)bytes, hipMemcpyDeviceToDeviceNoCU, (hipStream_t)stream));
+    return RT_OK;
+}
+
+// procedural::gpu::generate / SceneBuilder::build_gpu_scene put the scene on the device when it
+// is made (cube_world.cc:195-207, scene_builder.cu:29-81); the first update_scene then only
+// renders.  Here the upload is lazy (host-only scenes must load without a GPU), so a finished
+// scene on a machine with a gfx950 device is uploaded at once and one untimed 1-spp frame is
+// rendered into the device canvas: the code object, the scene's stream and the frame layout's
+// buffers (sky flags, live lists, scheduling history) are then in place before the caller's
+// first frame.  Without a usable device nothing happens (render calls report RT_ERR_NODEV as
+// before); a failure here is left for the first render to report.  RT_NO_WARM=1 turns it off.
+static int warm_scene(rt_scene* s);
+
 int rt_scene_load_json(const char* path, int width, int height, rt_scene** out) {
     if (!path || !out) return fail(RT_ERR_ARG, "null argument");
     std::unique_ptr<rt_scene> s(new rt_scene);
@@ -3653,6 +3693,7 @@ int rt_scene_load_json(const char* path, int width, int height, rt_scene** out) 
     if (r != 0) return fail(RT_ERR_PARSE, err);
     s->finished = true;
     s->canvas.assign((size_t)s->h.cam.W * s->h.cam.H, 0u);
+    (void)warm_scene(s.get());
     *out = s.release();
     return RT_OK;
 }
@@ -3760,6 +3801,7 @@ int rt_builder_finish(rt_scene* s, int W, int H, float fov, float unit, const fl
     if (s->h.flatten(&err) != 0) return fail(RT_ERR_PARSE, err);
     s->finished = true;
     s->canvas.assign((size_t)W * H, 0u);
+    (void)warm_scene(s);
     return RT_OK;
 }
 
@@ -4088,10 +4130,33 @@ int rt_update_scene(rt_scene* s, int kernel_dim, int optimize) {    // raytracer
     if (kernel_dim <= 0) return fail(RT_ERR_ARG, "kernel_dim must be positive");
     rt_render_opts o;
     rt_render_opts_default(&o);
-    o.use_bvh = optimize ? 1 : 0; o.rebuild_bvh = 1; o.kernel_dim = kernel_dim; o.sync = 1;
+    o.use_bvh = optimize ? 1 : 0; o.rebuild_bvh = 1; o.kernel_dim = kernel_dim;
+    o.sync = s->multi ? 1 : 0;                                // split frames end on the slot's streams
     int r = rt_render(s, &o, nullptr);
     if (r != RT_OK) return r;
-    HIPCHK(hipMemcpy(s->canvas.data(), s->d_canvas, s->canvas.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    // the canvas is host-readable on return (canvas.cu:23-29): one copy-engine transfer into the
+    // pinned host canvas on the frame's stream, then wait for that stream only
+    hipStream_t st = sstream(s);
+    if (s->canvas.pinned)
+        HIPCHK(hipMemcpyAsync(s->canvas.data(), s->d_canvas, s->canvas.size() * sizeof(uint32_t), hipMemcpyDeviceToDeviceNoCU, st));
+    else
+        HIPCHK(hipMemcpyAsync(s->canvas.data(), s->d_canvas, s->canvas.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return RT_OK;
+}
+
+static int warm_scene(rt_scene* s) {
+    static const bool off = [] { const char* e = getenv("RT_NO_WARM"); return e && atoi(e) != 0; }();
+    int n = 0;
+    if (off || hipGetDeviceCount(&n) != hipSuccess || n <= 0) { (void)hipGetLastError(); return RT_OK; }
+    const std::string saved = g_err;
+    rt_render_opts o;
+    rt_render_opts_default(&o);
+    o.sync = 1;
+    if (s->h.cam.W > 0 && s->h.cam.H > 0 && rt_render(s, &o, nullptr) != RT_OK) {
+        g_err = saved;                                    // left for the caller's first render to report
+        (void)hipGetLastError();
+    }
     return RT_OK;
 }
 

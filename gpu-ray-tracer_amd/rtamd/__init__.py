@@ -36,7 +36,7 @@ SYMBOLS = [
     "rt_canvas_get_color", "rt_debug_cast", "rt_kat_device", "rt_spp_offset", "rt_timing_collect",
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
     "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_scene_set_overlap", "rt_frame_work",
-    "rt_scene_set_devices", "rt_profile_marker",
+    "rt_scene_set_devices", "rt_profile_marker", "rt_host_alloc", "rt_host_free", "rt_copy_to_host_async",
 ]
 
 
@@ -141,6 +141,10 @@ def lib():
     L.rt_scene_set_devices.argtypes = [vp, vp, ip, ip]
     if hasattr(L, "rt_profile_marker"):         # (absent from libraries older than ABI 3's round 5: A/B runs)
         L.rt_profile_marker.argtypes = [ip, vp]
+    if hasattr(L, "rt_copy_to_host_async"):     # ABI 4
+        L.rt_host_alloc.argtypes = [ctypes.c_int64, ctypes.POINTER(vp)]
+        L.rt_host_free.argtypes = [vp]
+        L.rt_copy_to_host_async.argtypes = [vp, vp, ctypes.c_int64, vp]
     _lib = L
     return L
 
@@ -182,6 +186,42 @@ def profile_marker(tag, stream=None):
     default stream): tools/pmc_step.py finds a timed region between two markers."""
     if hasattr(lib(), "rt_profile_marker"):
         _check(lib().rt_profile_marker(int(tag), stream))
+
+
+class HostBuffer:
+    """Pinned host memory from rt_host_alloc (hipHostMalloc), viewed as a torch / numpy array.
+    The frame's host copy lands here through a copy engine (copy_to_host_async)."""
+
+    def __init__(self, shape, dtype=np.int32):
+        self.shape, self.dtype = tuple(shape), np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = ctypes.c_void_p()
+        _check(lib().rt_host_alloc(self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr)) \
+            .view(self.dtype).reshape(self.shape)
+
+    def tensor(self):
+        import torch
+        return torch.from_numpy(self.array)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            _check(lib().rt_host_free(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def copy_to_host_async(host_ptr, dev_ptr, nbytes, stream=None):
+    """Device -> pinned-host copy on a DMA copy engine, enqueued on `stream` (an int
+    hipStream_t; None = the null stream).  No CU is used (rt_copy_to_host_async)."""
+    _check(lib().rt_copy_to_host_async(host_ptr, dev_ptr, int(nbytes), stream))
 
 
 def material(Ke=(0, 0, 0, 0), Ka=(0, 0, 0, 0), Kd=(0, 0, 0, 0), Ks=(0, 0, 0, 0), Kt=(0, 0, 0, 0), Kr=(0, 0, 0, 0),

@@ -123,17 +123,27 @@ class FramePipeline:
 
     readback=True keeps the reference's post-condition (update_scene returns with the frame
     host-readable, raytracer.cu:102-120 / canvas.cu:23-29) without giving up the overlap: the
-    finished frame (rank 0) is copied into pinned host buffer k % host_buffers by an
-    asynchronous device-to-host copy -- on the render stream for one rank, on a copy stream
-    after the un-permute otherwise -- while later frames render.  `host_frame(k)` waits for
-    frame k's copy; a host buffer is reused host_buffers frames later, after its copy (and the
-    caller's read) is done, so a consumer may read frames up to host_buffers - 1 behind the
-    last one issued.  host_buffers defaults to 2 x depth: the frames the consumer has not read
-    yet are the frames in flight, and a consumer only depth - 1 behind caps them at depth
-    including the copies (measured: DESIGN.md §4.1)."""
+    finished frame (rank 0) is copied into pinned host buffer k % host_buffers (rt_host_alloc)
+    by a copy-engine transfer (rt_copy_to_host_async: no blit kernel, no CU taken from the
+    frames in flight) -- on the render stream for one rank, on a copy stream after the
+    un-permute otherwise -- while later frames render.  `host_frame(k)` waits for frame k's
+    copy; a host buffer is reused host_buffers frames later, after its copy (and the caller's
+    read) is done, so a consumer may read frames up to host_buffers - 1 behind the last one
+    issued.  host_buffers defaults to 2 x depth: the frames the consumer has not read yet are
+    the frames in flight, and a consumer only depth - 1 behind caps them at depth including the
+    copies (measured: DESIGN.md §4.1).
+
+    host_staging=True (device frames, a backend without device tensors: gloo, several ranks
+    sharing one GPU in the tests of bench.py's N > 1 path): each rank's slice is copied by the
+    copy engine into a pinned staging buffer per slot on the render stream, and frame k's gather
+    of those host slices is issued when frame k + 1 has been issued (after a host wait for frame
+    k's staging copy, so that frames k and k + 1 are in flight meanwhile); rank 0 uploads the
+    gathered slices into the slot's device gather buffer and un-permutes there as the RCCL path
+    does.  The per-slot waits are those of the RCCL path: a slot's staging buffer is rewritten
+    after its previous gather has completed, its gather buffer after its previous un-permute."""
 
     def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False,
-                 streams=None, host_buffers=None):
+                 streams=None, host_buffers=None, host_staging=False):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
@@ -155,6 +165,16 @@ class FramePipeline:
         self.main = torch.cuda.current_stream(device) if self.cuda else None
         self.gbufs = ([torch.empty((world, self.rows, width), dtype=dtype, device=device) for _ in range(D)]
                       if (world > 1 and rank == 0) else None)
+        self.host_staging = bool(host_staging) and world > 1 and self.cuda
+        self.np_dtype = torch.empty(0, dtype=dtype).numpy().dtype
+        if self.host_staging:
+            from . import HostBuffer
+            self._stage = [HostBuffer((self.rows, width), self.np_dtype) for _ in range(D)]
+            self.stage = [b.tensor() for b in self._stage]
+            self.stage_ev = [None] * D          # staging copy of the frame last rendered in each slot
+            self.hgbufs = ([torch.empty((world, self.rows, width), dtype=dtype) for _ in range(D)]
+                           if rank == 0 else None)
+            self.stage_pending = None           # (frame, slot) staged but not yet gathered
         self.readback = bool(readback) and (world == 1 or rank == 0)
         n_out = D if self.readback else 1                 # one un-permute target per slot when copied out
         self.outs = ([torch.empty((height, width), dtype=dtype, device=device) for _ in range(n_out)]
@@ -162,7 +182,12 @@ class FramePipeline:
         self.out = self.outs[0] if self.outs else None
         self.n_host = max(D, int(host_buffers)) if host_buffers else 2 * D
         if self.readback:
-            self.host = [torch.empty((height, width), dtype=dtype, pin_memory=self.cuda) for _ in range(self.n_host)]
+            if self.cuda:                       # pinned by the library: the copy engine writes it
+                from . import HostBuffer
+                self._host = [HostBuffer((height, width), self.np_dtype) for _ in range(self.n_host)]
+                self.host = [b.tensor() for b in self._host]
+            else:
+                self.host = [torch.empty((height, width), dtype=dtype) for _ in range(self.n_host)]
             self.host_ev = [None] * self.n_host     # D2H copy of the frame last copied into each host buffer
             self.host_no = [-1] * self.n_host       # its frame number
             self.out_copy = [None] * D              # world > 1: the copy that last read each un-permute target
@@ -196,7 +221,13 @@ class FramePipeline:
         if self.host_ev[h] is not None:
             self.host_ev[h].synchronize()           # frame k - n_host's copy is done (and was read)
         with self._on(stream):
-            self.host[h].copy_(src, non_blocking=self.cuda)
+            if self.cuda:
+                from . import copy_to_host_async
+                assert src.is_contiguous()
+                copy_to_host_async(self._host[h].ptr, src.data_ptr(), src.numel() * src.element_size(),
+                                   stream.cuda_stream)
+            else:
+                self.host[h].copy_(src)
             ev = self._event(stream)
         self.host_ev[h], self.host_no[h] = ev, k
         return ev
@@ -209,6 +240,8 @@ class FramePipeline:
             self.work[s].wait()
             if self.rank == 0:
                 g = self.gbufs[s]
+                if self.host_staging:           # the gathered host slices -> the slot's device gather buffer
+                    g.copy_(self.hgbufs[s])
                 out = self.outs[s % len(self.outs)]
                 if self.readback and self.out_copy[s] is not None and self.cuda:
                     self.main.wait_event(self.out_copy[s])  # frame k - depth's copy has read out
@@ -225,10 +258,36 @@ class FramePipeline:
                         self.copy_stream.wait_event(ev)
                     self.out_copy[s] = self._to_host(self.pend_no[s], out, self.copy_stream)
 
+    def _gather_staged(self):
+        """host_staging: issue the gather of the frame staged last (after its staging copy)."""
+        if self.stage_pending is None:
+            return
+        k, s = self.stage_pending
+        self.stage_pending = None
+        self.stage_ev[s].synchronize()
+        gl = list(self.hgbufs[s].unbind(0)) if self.rank == 0 else None
+        self.work[s] = self.dist.gather(self.stage[s], gl, dst=0, async_op=True)
+        self.pending[s] = True
+        self.pend_no[s] = k
+
     def step(self, k, render):
         """Issue frame k: render(part, stream) enqueues the render of this rank's rows."""
         s = k % self.depth
         st = self.streams[s]
+        if self.host_staging:
+            with self._on(st):
+                if self.work[s] is not None:
+                    self.work[s].wait()                 # frame k-depth's gather has read stage[s]
+                render(self.parts[s], st)
+                from . import copy_to_host_async
+                copy_to_host_async(self._stage[s].ptr, self.parts[s].data_ptr(), self._stage[s].nbytes, st.cuda_stream)
+                self.stage_ev[s] = self._event(st)
+            self._gather_staged()                       # frame k - 1's gather (frame k is in flight)
+            self.stage_pending = (k, s)
+            if k >= 1:
+                self._unpermute((k - 1) % self.depth)
+            self.last = k
+            return
         with self._on(st):
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
@@ -250,6 +309,8 @@ class FramePipeline:
         """Frame k on the host (readback=True; rank 0): waits for its device-to-host copy.
         Valid until frame k + host_buffers is issued."""
         s = k % self.depth
+        if self.host_staging and self.stage_pending is not None and self.stage_pending[0] == k:
+            self._gather_staged()
         if self.world > 1 and self.pending[s] and self.pend_no[s] == k:
             self._unpermute(s)
         h = k % self.n_host
@@ -259,6 +320,8 @@ class FramePipeline:
 
     def finish(self):
         """Complete every issued frame (stream-ordered on the main stream)."""
+        if self.host_staging:
+            self._gather_staged()
         for s in range(self.depth):
             self._unpermute(s)
         if self.cuda:

@@ -23,8 +23,10 @@ extern "C" {
 #endif
 
 /* 3: rt_work gained the query-occupancy fields; RT_EXPORT_TRIS / RT_EXPORT_TEXCOORDS list
- *    triangles in the flattened mesh order (the index space of hit_tri) */
-#define RT_ABI_VERSION 3
+ *    triangles in the flattened mesh order (the index space of hit_tri)
+ * 4: rt_host_alloc / rt_host_free / rt_copy_to_host_async (host-readable frames through a copy
+ *    engine); a finished scene is uploaded and warmed at creation when a gfx950 device is present */
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -46,7 +48,13 @@ int rt_device_count(int* count);
 /* Select the HIP device for subsequent scene uploads on this thread. */
 int rt_set_device(int device);
 
-/* ---- scene creation (host only; device upload is lazy, at first render) ---- */
+/* ---- scene creation ----
+ * A finished scene (rt_scene_load_json, rt_builder_finish) goes to the current device at once
+ * when a gfx950 device is present, as procedural::gpu::generate / build_gpu_scene do
+ * (cube_world.cc:195-207, scene_builder.cu:29-81), and one untimed 1-spp frame warms the code
+ * object, the scene's stream and the frame buffers; the first rt_update_scene then only renders.
+ * Without a device the scene stays host-only and render calls return RT_ERR_NODEV.
+ * RT_NO_WARM=1 (environment) defers the upload to the first render. */
 /* worldN.json -> scene (cube_world.cc:38-191).  width/height <= 0 keep the JSON's canvas size. */
 int rt_scene_load_json(const char* path, int width, int height, rt_scene** out);
 /* Empty scene for the builder API (SceneBuilder{atlas_path}, scene_builder.h:51-56). */
@@ -211,8 +219,20 @@ int rt_scene_set_devices(rt_scene* s, const int* devices, int n_devices, int n_r
  * since the last collect (synchronizes those events), then resets. */
 int rt_timing_collect(rt_scene* s, double* bvh_ms_total, double* trace_ms_total, int* n_frames);
 
-/* Reference-equivalent frame: rebuild BVH if optimize, trace 1 spp, synchronize,
- * framebuffer host-readable afterwards (raytracer.cu:102-120). */
+/* ---- host-readable frames (the post-condition of update_scene, raytracer.cu:102-120 /
+ * canvas.cu:23-29: the canvas is host memory the caller reads after the call) ---- */
+/* Pinned (page-locked) host memory: the copy engines write it directly over PCIe. */
+int rt_host_alloc(int64_t bytes, void** out);
+int rt_host_free(void* p);
+/* Enqueue a device -> host copy of `bytes` on `stream` (a hipStream_t; NULL = the null stream)
+ * on a DMA copy engine: no compute unit is taken from frames in flight.  host_dst should come
+ * from rt_host_alloc (pageable memory is staged by the runtime).  Stream-ordered: record an
+ * event after it, or synchronize the stream, before reading host_dst. */
+int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
+
+/* Reference-equivalent frame: rebuild BVH if optimize, trace 1 spp, copy the frame into the
+ * pinned host canvas on a copy engine, wait for that stream; the framebuffer is host-readable
+ * afterwards (raytracer.cu:102-120). */
 int rt_update_scene(rt_scene* s, int kernel_dim, int optimize);
 /* Host framebuffer (RGBA8 packed R<<24|G<<16|B<<8|A, row-major W*H) after rt_update_scene. */
 int rt_canvas_read(const rt_scene* s, uint32_t* dst, int64_t n_pixels);

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(rt):
 
 
 def test_abi_version(rt):
-    assert rt.lib().rt_abi_version() == 3
+    assert rt.lib().rt_abi_version() == 4
 
 
 def test_library_is_gfx950_code(rt):
@@ -91,3 +91,16 @@ def test_overlap_policy_arguments(rt):
     s.set_overlap(False)
     for bad in (3, -1):
         assert rt.lib().rt_scene_set_overlap(s._h, bad) == rt.RT_ERR_ARG
+
+
+def test_host_copy_entries_without_gpu(rt):
+    """ABI 4's host-readable frame entries: argument checks, and no pinned memory without a GPU
+    (no CPU stand-in: the copy is a copy-engine transfer or nothing)."""
+    L = rt.lib()
+    assert L.rt_copy_to_host_async(None, None, 16, None) == rt.RT_ERR_ARG
+    p = ctypes.c_void_p()
+    assert L.rt_host_alloc(0, ctypes.byref(p)) == rt.RT_ERR_ARG
+    assert L.rt_host_free(None) == rt.RT_OK
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is present")
+    assert L.rt_host_alloc(4096, ctypes.byref(p)) == rt.RT_ERR_NODEV

@@ -33,9 +33,12 @@ def stress_1080p(oracle):
     return oracle.render(oracle.load(scene_path("world8_stress"), W, H), spp=8, nthreads=NTHREADS)
 
 
-def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=False, size=(W, H), stream=True):
+def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=False, size=(W, H), stream=True,
+               host=False):
     """This rank's rows of the last of n_frames frames issued as bench.py issues them (its timed
-    frames: RT_OVERLAP_STREAM)."""
+    frames: RT_OVERLAP_STREAM).  host=True: the frames as bench.py's headline times them, each
+    copied by a copy engine into pinned host memory and read there by a consumer that trails the
+    pipeline (FramePipeline(readback=True)): the list of every frame's host copy."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
     import rtamd.dist as rtdist
@@ -45,21 +48,34 @@ def _pipelined(gpu, scene, spp, world=1, rank=0, depth=8, n_frames=11, textures=
         s.load_atlas()
     s.set_frame_slots(depth)
     s.set_overlap(False, stream=stream)
-    pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", depth=depth)
+    pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", depth=depth, readback=host)
+    n = len(range(rank, H, world))
+    frames = []
     for k in range(n_frames):
         pipe.step(k, lambda buf, st: s.render_device(spp=spp, row0=rank, row_step=world, compact=True,
                                                      rgba_ptr=buf.data_ptr(), stream=st.cuda_stream,
                                                      textures=textures))
+        if host and k - pipe.n_host + 1 >= 0:
+            frames.append(pipe.host_frame(k - pipe.n_host + 1)[:n].numpy().view(np.uint32).copy())
     out = pipe.finish()
     torch.cuda.synchronize()
-    return out[:len(range(rank, H, world))].cpu().numpy().view(np.uint32)
+    if host:
+        for j in range(max(0, n_frames - pipe.n_host + 1), n_frames):
+            frames.append(pipe.host_frame(j)[:n].numpy().view(np.uint32).copy())
+        assert len(frames) == n_frames
+        return frames
+    return out[:n].cpu().numpy().view(np.uint32)
 
 
 def test_bench_frame_world8_stress_1080p(gpu, stress_1080p):
-    """The headline frame: pipelined fast frames (RGBA8 as the bench keeps it), then one fast
+    """The headline frame: pipelined fast frames as the bench times them (each copied to pinned
+    host memory by a copy engine and read from there; every one of them checked), then one fast
     frame with every output, against the oracle."""
+    host = _pipelined(gpu, "world8_stress", 8, n_frames=20, host=True)
+    for k, f in enumerate(host):
+        assert_frames_equal({"rgba": f}, stress_1080p, keys=("rgba",), ctx="host frame %d" % k)
     rgba = _pipelined(gpu, "world8_stress", 8)
-    assert_frames_equal({"rgba": rgba}, stress_1080p, keys=("rgba",), ctx="pipelined")
+    assert np.array_equal(rgba, host[-1])
     s = gpu.Scene.load_json(scene_path("world8_stress"), W, H)
     fr = s.render(spp=8, want=WANT, stats=False)
     assert np.array_equal(fr["rgba"], rgba)

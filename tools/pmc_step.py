@@ -102,7 +102,15 @@ def main():
     if os.path.exists(kt_log):
         for line in open(kt_log):
             if line.startswith("{") and '"ms_per_step"' in line:
-                entry["profiled_ms_per_step"] = json.loads(line)["ms_per_step"]
+                d = json.loads(line)
+                entry["profiled_ms_per_step"] = d["ms_per_step"]
+                # the kind of window profiled: bench.py flags per_step figures from another kind
+                entry["window"] = {
+                    "grid_timed_frames": d.get("config", {}).get("grid_timed_frames"),
+                    "frames_in_flight": d.get("frames_in_flight"),
+                    "timed_to": ("host" if str(d.get("timed_to", "")).startswith("host") else "device")
+                                if d.get("frames_in_flight", 1) > 1 else "serial",
+                    "lib_sha16": d.get("build", {}).get("lib_sha16")}
     if b:
         entry["gpu_busy_ms_per_step"] = b["busy_ns"] / steps / 1e6
         entry["window_span_ms"] = b["span_ns"] / 1e6
