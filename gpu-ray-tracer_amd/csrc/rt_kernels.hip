@@ -2808,7 +2808,18 @@ int ensure_other_slot(rt_scene* s) {
         HIPCHK(hipMalloc((void**)&o.d_inst4, std::max<size_t>(1, s->h.d_insts.size()) * sizeof(float4)));
         // the grid-wide build's sort buffers now, not at the slot's first frame inside a pipeline
         if (s->n_leaf > BVH_WG_LEAVES && !o.d_bscratch) HIPCHK(hipMalloc(&o.d_bscratch, bvh_large_scratch_bytes(s->n_leaf)));
-        o.slot_inst_gen = 0;                                 // filled by sync_slot_insts on first use
+        // the current poses now (blocking copies, here rather than at the slot's first frame: an
+        // asynchronous copy on a frame's stream may start a new SDMA engine, ~7 ms of host time
+        // the first time, profiles/r06/rblog/); later pose changes reach the slot through
+        // sync_slot_insts, stream-ordered
+        const size_t n = s->h.d_insts.size();
+        if (n) {
+            std::vector<float4> v4(n);
+            fill_inst4(s->h, v4.data());
+            HIPCHK(hipMemcpy(o.d_insts, s->h.d_insts.data(), n * sizeof(DInst), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(o.d_inst4, v4.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+        }
+        o.slot_inst_gen = s->inst_gen;
         o.work_zeroed = false; o.bvh_valid = false;
     }
     return mirror_slot_caps(s);                              // the current slot's grown buffers too
@@ -3631,6 +3642,15 @@ int rt_set_device(int device) {
 // rocprofv3 trace where a caller's timed region begins and ends (tools/pmc_step.py).
 namespace {
 __global__ __launch_bounds__(64) void profile_marker_kernel(int tag) { (void)tag; }
+
+// rt_copy_engines_warm's gate: one wave that holds the copies queued behind it pending until the
+// host opens the gate (a flag in coherent host memory) or `max_ticks` of the wall clock pass, so
+// that every queued copy finds the engines of the copies before it busy.  Vector loads only.
+__global__ __launch_bounds__(64) void copy_gate_kernel(const unsigned* flag, unsigned long long max_ticks) {
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u && wall_clock64() - t0 < max_ticks)
+        __builtin_amdgcn_s_sleep(32);
+}
 }  // namespace
 
 int rt_profile_marker(int tag, void* stream) {
@@ -3671,6 +3691,54 @@ int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, vo
     if (!host_dst || !dev_src || bytes < 0) return fail(RT_ERR_ARG, "null pointer or negative size");
     if (bytes == 0) return RT_OK;
     HIPCHK(hipMemcpyAsync(host_dst, dev_src, (size_t)bytes, hipMemcpyDeviceToDeviceNoCU, (hipStream_t)stream));
+    return RT_OK;
+}
+
+// The runtime gives a copy an idle SDMA engine, keeping a stream on its last engine only while
+// nothing else was ordered in between; a pipeline's copies queue behind frames still rendering,
+// so the k-th pending copy lands on the k-th engine, and the first copy on an engine creates
+// that engine's queue: ~7 ms of host time inside hipMemcpyAsync (profiles/r06/rblog2/).  Here n
+// copies are queued on `stream` behind a gate kernel on a second stream, each after a wait on
+// the gate, so each finds the engines before it busy and starts the next one; then the gate
+// opens.  Once per process and device (later calls return at once).
+int rt_copy_engines_warm(void* stream, int n) {
+    if (n < 1 || n > 64) return fail(RT_ERR_ARG, "engines: 1 to 64");
+    int ndev = 0, dev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
+    HIPCHK(hipGetDevice(&dev));
+    static std::mutex mu;
+    static int warmed[64] = {};
+    std::lock_guard<std::mutex> lock(mu);
+    if (dev < 0 || dev >= 64 || warmed[dev] >= n) return RT_OK;
+    unsigned* flag = nullptr; uint8_t* h = nullptr; uint8_t* d = nullptr;
+    hipStream_t gate = nullptr; hipEvent_t ev = nullptr;
+    int clk_khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, dev));
+    HIPCHK(hipHostMalloc((void**)&flag, 4, hipHostMallocCoherent));
+    // (copies below the runtime's SDMA threshold run elsewhere: 1 MB each, all into one buffer)
+    constexpr size_t B = 1 << 20;
+    HIPCHK(hipHostMalloc((void**)&h, B, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&d, B));
+    HIPCHK(hipMemset(d, 0, B));
+    HIPCHK(hipStreamCreateWithFlags(&gate, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(copy_gate_kernel, dim3(1), dim3(64), 0, gate, (const unsigned*)flag,
+                       (unsigned long long)clk_khz * 2000ull);                     // at most 2 s
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev, gate));
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; i++) {
+        e = hipStreamWaitEvent((hipStream_t)stream, ev, 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, B, hipMemcpyDeviceToDeviceNoCU, (hipStream_t)stream);
+    }
+    __atomic_store_n(flag, 1u, __ATOMIC_RELEASE);                              // open the gate
+    HIPCHK(hipStreamSynchronize(gate));
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    HIPCHK(e);
+    (void)hipEventDestroy(ev); (void)hipStreamDestroy(gate);
+    (void)hipFree(d); (void)hipHostFree(h); (void)hipHostFree(flag);
+    warmed[dev] = n;
     return RT_OK;
 }
 

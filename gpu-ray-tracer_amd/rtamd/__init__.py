@@ -37,6 +37,7 @@ SYMBOLS = [
     "rt_builder_add_triangle_tex", "rt_builder_build_cube_tex", "rt_scene_set_atlas", "rt_scene_load_atlas",
     "rt_scene_atlas_info", "rt_scene_set_frame_slots", "rt_scene_set_overlap", "rt_frame_work",
     "rt_scene_set_devices", "rt_profile_marker", "rt_host_alloc", "rt_host_free", "rt_copy_to_host_async",
+    "rt_copy_engines_warm",
 ]
 
 
@@ -145,6 +146,7 @@ def lib():
         L.rt_host_alloc.argtypes = [ctypes.c_int64, ctypes.POINTER(vp)]
         L.rt_host_free.argtypes = [vp]
         L.rt_copy_to_host_async.argtypes = [vp, vp, ctypes.c_int64, vp]
+        L.rt_copy_engines_warm.argtypes = [vp, ip]
     _lib = L
     return L
 
@@ -222,6 +224,11 @@ def copy_to_host_async(host_ptr, dev_ptr, nbytes, stream=None):
     """Device -> pinned-host copy on a DMA copy engine, enqueued on `stream` (an int
     hipStream_t; None = the null stream).  No CU is used (rt_copy_to_host_async)."""
     _check(lib().rt_copy_to_host_async(host_ptr, dev_ptr, int(nbytes), stream))
+
+
+def copy_engines_warm(stream=None, n=16):
+    """Start n SDMA engines from `stream` ahead of a host-copy pipeline (rt_copy_engines_warm)."""
+    _check(lib().rt_copy_engines_warm(stream, int(n)))
 
 
 def material(Ke=(0, 0, 0, 0), Ka=(0, 0, 0, 0), Kd=(0, 0, 0, 0), Ks=(0, 0, 0, 0), Kt=(0, 0, 0, 0), Kr=(0, 0, 0, 0),

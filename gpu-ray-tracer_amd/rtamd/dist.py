@@ -191,7 +191,17 @@ class FramePipeline:
             self.host_ev = [None] * self.n_host     # D2H copy of the frame last copied into each host buffer
             self.host_no = [-1] * self.n_host       # its frame number
             self.out_copy = [None] * D              # world > 1: the copy that last read each un-permute target
-            self.copy_stream = torch.cuda.Stream(device=device) if (world > 1 and self.cuda) else None
+            # Every host copy on ONE copy stream, after an event of the frame's stream.  The runtime
+            # keeps a stream's copies on the SDMA engine it used last and gives a stream with no
+            # copy history the first idle engine; the first copy on an engine creates its queue
+            # (~7 ms on the host, profiles/r06/rblog/).  Copies from eight render streams spread
+            # over new engines inside the timed window (1.2 ms per frame against 0.67 device-
+            # resident, profiles/r06/rbprobe/); one stream keeps them on one engine.
+            self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
+            self.copy_done = [None] * D             # one rank: the copy that last read parts[s]
+            if self.cuda:                           # the engines the pending copies will spread over
+                from . import copy_engines_warm
+                copy_engines_warm(self.copy_stream.cuda_stream, 16)
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
         self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
@@ -291,9 +301,13 @@ class FramePipeline:
         with self._on(st):
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
+            if self.readback and self.world == 1 and self.cuda and self.copy_done[s] is not None:
+                st.wait_event(self.copy_done[s])        # frame k-depth's host copy has read parts[s]
             render(self.parts[s], st)
             if self.readback and self.world == 1:
-                self._to_host(k, self.parts[s], st)
+                if self.cuda:
+                    self.copy_stream.wait_event(self._event(st))
+                self.copy_done[s] = self._to_host(k, self.parts[s], self.copy_stream)
             if self.world > 1:
                 if self.unperm[s] is not None and self.cuda:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]

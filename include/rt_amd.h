@@ -24,8 +24,8 @@ extern "C" {
 
 /* 3: rt_work gained the query-occupancy fields; RT_EXPORT_TRIS / RT_EXPORT_TEXCOORDS list
  *    triangles in the flattened mesh order (the index space of hit_tri)
- * 4: rt_host_alloc / rt_host_free / rt_copy_to_host_async (host-readable frames through a copy
- *    engine); a finished scene is uploaded and warmed at creation when a gfx950 device is present */
+ * 4: rt_host_alloc / rt_host_free / rt_copy_to_host_async / rt_copy_engines_warm (host-readable
+ *    frames through a copy engine); a finished scene is uploaded and warmed at creation when a gfx950 device is present */
 #define RT_ABI_VERSION 4
 
 enum {
@@ -229,6 +229,12 @@ int rt_host_free(void* p);
  * from rt_host_alloc (pageable memory is staged by the runtime).  Stream-ordered: record an
  * event after it, or synchronize the stream, before reading host_dst. */
 int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
+/* Start n of the device's SDMA copy engines from `stream` (the stream a pipeline's host copies
+ * will use), once per process and device.  The runtime hands a copy queued while earlier copies
+ * are still pending the next idle engine, and a copy's first use of an engine creates that
+ * engine's queue (~7 ms of host time inside the enqueue): a pipeline with frames in flight would
+ * pay that inside its first frames.  Blocks until done; later calls return at once. */
+int rt_copy_engines_warm(void* stream, int n_engines);
 
 /* Reference-equivalent frame: rebuild BVH if optimize, trace 1 spp, copy the frame into the
  * pinned host canvas on a copy engine, wait for that stream; the framebuffer is host-readable

@@ -443,6 +443,99 @@ def test_brute_sky_prepass_grazing(gpu, oracle, scene, spp, row_step):
     assert n > 50 and skies < n
 
 
+def _opaque_cubes(gpu, oracle, w, h):
+    """A built opaque scene of 12 cube instances (3 meshes: diffuse, specular, mirror) on a
+    ragged grid: the brute-force sky pre-pass tests every instance's grown box (<= 64)."""
+    m = gpu.material
+    mats = [m(Ka=(0.1, 0.1, 0.1, 1), Kd=(0.6, 0.3, 0.1, 1)),
+            m(Ka=(0.1, 0.1, 0.1, 1), Kd=(0.2, 0.5, 0.2, 1), Ks=(0.8, 0.8, 0.8, 1), alpha=6.0),
+            m(Kd=(0.3, 0.3, 0.3, 1), Ks=(0.5, 0.5, 0.5, 1), Kr=(0.7, 0.7, 0.7, 1), alpha=8.0)]
+    t = Twin(gpu, oracle)
+    meshes = [t.build_cube(1.0, mt) for mt in mats]
+    rng = np.random.default_rng(11)
+    for i in range(4):
+        for j in range(3):
+            k = t.add_trans(meshes[(i + j) % 3])
+            t.set_trans(k, pos=(2.5 * i - 3.75 + float(rng.uniform(-0.3, 0.3)), float(rng.integers(0, 3)),
+                                3.0 * j - 3.0))
+    t.add_point_light((0.5, 6.0, 0.3), (1.0, 1.0, 1.0, 1.0))
+    t.add_directional_light((0.3, -1.0, 0.8), (0.9, 0.8, 0.7, 1.0))
+    t.finish(w, h, 60.0, 100.0, cam_pos=(0.0, 9.0, -12.0), cam_quat=(-0.3826834, 0.0, 0.0, 0.9238795),
+             dist_atten=(0.1, 0.05, 0.01), ambience=(0.2, 0.2, 0.2, 1.0), depth=3)
+    return t.gpu, t.orc
+
+
+@pytest.mark.parametrize("scene,spp,row_step", [("world8", 1, 1), ("world8", 8, 3), ("world8_stress", 2, 1),
+                                                ("world8_stress", 8, 8), ("cubes", 1, 1), ("cubes", 8, 2)])
+def test_brute_fast_opaque(gpu, oracle, scene, spp, row_step):
+    """the opaque brute-force kernel (trace_kernel<0, true, M_BRUTE | ...>, NS = 0: no
+    refraction code, the occlusion early exit `b.time <= occl_t`) on opaque scenes -- world8 (380
+    instances) and world8_stress (570; both above the sky pre-pass's 64) and the built 12-instance
+    scene (with the brute-force sky pre-pass) -- fast == counted bit for bit == the oracle's
+    use_bvh = 0 frame, whole frames and row slices, from the scene's camera and two others."""
+    w, h = 96, 64
+    if scene == "cubes":
+        s, o = _opaque_cubes(gpu, oracle, w, h)
+    else:
+        s = gpu.Scene.load_json(scene_path(scene), w, h)
+        o = oracle.load(scene_path(scene), w, h)
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    poses = [None, ((1.0, 6.0, -8.0), (-0.2588190, 0.0, 0.0, 0.9659258)), ((-4.0, 2.0, 3.0), (0.0, 0.7071068, 0.0, 0.7071068))]
+    hits = 0
+    for pose in poses:
+        if pose:
+            s.set_camera(*pose)
+        kw = dict(spp=spp, use_bvh=False, want=want, row0=row_step - 1, row_step=row_step, compact=True)
+        fast = s.render(stats=False, **kw)
+        full = s.render(stats=True, **kw)
+        for k in want:
+            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (pose, k)
+        mirror_camera(s, o)
+        orc_check(oracle, o, fast, spp, row0=row_step - 1, row_step=row_step, compact=True, use_bvh=0, ctx=(scene, pose))
+        hits += int((full["hit_inst"] >= 0).sum())
+    assert hits > 0
+
+
+@pytest.mark.parametrize("spp,row_step", [(1, 1), (4, 3)])
+def test_brute_sky_prepass_grazing_many(gpu, oracle, spp, row_step):
+    """the brute-force sky pre-pass over many instances (the built 12-cube opaque
+    scene; world1 has two): cameras on, beside and away from the face planes of six instance
+    boxes, looking along them and across, so that rays pass within rounding of several grown
+    boxes at once; fast (pre-pass) == counted (none) bit for bit == the oracle."""
+    w, h = 48, 32
+    s, o = _opaque_cubes(gpu, oracle, w, h)
+    v = s.export("vertices")
+    inst = s.export("instances")
+    c, sn = np.cos, np.sin
+    quats = [(0.0, 0.0, 0.0, 1.0)]
+    for a in (0.5, 1.0, 1.5):
+        quats.append((0.0, float(sn(0.5 * np.pi * a)), 0.0, float(c(0.5 * np.pi * a))))
+    quats.append((float(sn(-0.125 * np.pi)), 0.0, 0.0, float(c(-0.125 * np.pi))))
+    want = ("rgba", "radiance", "hit_inst", "hit_tri")
+    n = skies = 0
+    for i in range(0, len(inst), 2):
+        lo, hi = inst[i, 4:7] + v.min(0), inst[i, 4:7] + v.max(0)
+        mid = 0.5 * (lo + hi)
+        for axis in range(3):
+            for side, plane in ((0, lo[axis]), (1, hi[axis])):
+                for off in (0.0, 1e-3, 3.0):
+                    pos = mid.copy()
+                    pos[axis] = plane + (off if side else -off)
+                    for q in quats[:: (1 if axis == 1 else 2)]:
+                        s.set_camera([float(x) for x in pos], q)
+                        kw = dict(spp=spp, use_bvh=False, want=want, row0=row_step - 1, row_step=row_step, compact=True)
+                        fast = s.render(stats=False, **kw)
+                        full = s.render(stats=True, **kw)
+                        for k in want:
+                            assert np.array_equal(fast[k].view(np.uint32), full[k].view(np.uint32)), (i, axis, side, off, q, k)
+                        mirror_camera(s, o)
+                        orc_check(oracle, o, fast, spp, row0=row_step - 1, row_step=row_step, compact=True, use_bvh=0,
+                                  ctx=(i, axis, side, off, q))
+                        n += 1
+                        skies += int((full["hit_inst"] < 0).all())
+    assert n > 100 and skies < n
+
+
 @pytest.mark.parametrize("col1", [(0.9, 0.8, 0.7, 1.0), (0.9, -0.0, 0.7, 1.0)])
 def test_unlit_skip_exact(gpu, oracle, col1):
     """The fast kernels trace no shadow segments for a light whose phong factor (diffuse +

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Host issue and wait times of the host-readable frame pipeline (bench.py's headline loop):
+per frame, how long the host spends issuing it (FramePipeline.step) and waiting for the frame
+it reads (host_frame), and the loop's ms per frame; host-readable (copies on one copy stream)
+and device-resident for comparison."""
+import json
+import os
+import sys
+import time
+
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "16")
+import torch  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ray-tracer_amd"))
+import rtamd  # noqa: E402
+import rtamd.dist as rtdist  # noqa: E402
+
+
+def main():
+    readback = (sys.argv[1] if len(sys.argv) > 1 else "1") == "1"
+    n = 40
+    W, H, D = 1920, 1080, 8
+    pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", None, depth=D, readback=readback)
+    for st in pipe.streams + ([pipe.copy_stream] if readback else []):
+        torch.cuda.Event().record(st)
+    scene = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", "world8_stress.json"), W, H)
+    scene.set_frame_slots(D)
+    torch.cuda.synchronize()
+
+    def render(buf, st):
+        scene.render_device(spp=8, rgba_ptr=buf.data_ptr(), stream=st.cuda_stream)
+    for k in range(10):
+        pipe.step(k, render)
+    pipe.finish()
+    torch.cuda.synchronize()
+    scene.set_overlap(False, stream=True)
+    issue, wait = [], []
+    t0 = time.perf_counter()
+    for i in range(n):
+        k = 10 + i
+        a = time.perf_counter()
+        pipe.step(k, render)
+        b = time.perf_counter()
+        if readback and k - pipe.n_host + 1 >= 10:
+            pipe.host_frame(k - pipe.n_host + 1)
+        c = time.perf_counter()
+        issue.append((b - a) * 1e3)
+        wait.append((c - b) * 1e3)
+    pipe.finish()
+    if readback:
+        pipe.host_frame(10 + n - 1)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n * 1e3
+    scene.set_overlap(False)
+    print(json.dumps({"readback": readback, "ms_per_frame": round(dt, 4),
+                      "issue_ms": [round(x, 3) for x in issue], "wait_ms": [round(x, 3) for x in wait]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
