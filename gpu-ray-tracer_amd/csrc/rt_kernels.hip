@@ -3694,15 +3694,16 @@ int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, vo
     return RT_OK;
 }
 
-// The runtime gives a copy an idle SDMA engine, keeping a stream on its last engine only while
-// nothing else was ordered in between; a pipeline's copies queue behind frames still rendering,
-// so the k-th pending copy lands on the k-th engine, and the first copy on an engine creates
-// that engine's queue: ~7 ms of host time inside hipMemcpyAsync (profiles/r06/rblog2/).  Here n
-// copies are queued on `stream` behind a gate kernel on a second stream, each after a wait on
-// the gate, so each finds the engines before it busy and starts the next one; then the gate
-// opens.  Once per process and device (later calls return at once).
-int rt_copy_engines_warm(void* stream, int n) {
-    if (n < 1 || n > 64) return fail(RT_ERR_ARG, "engines: 1 to 64");
+// The runtime gives a stream's first copy (and a copy after the stream's last one has drained)
+// an idle SDMA engine, and keeps the stream on that engine otherwise; a pipeline's copies queue
+// behind frames still rendering, so as they pile up they land on engines 1, 2, 4, ... and the
+// first copy on an engine in a direction creates that engine's queue: ~7 ms of host time inside
+// hipMemcpyAsync (profiles/r06/rblog/).  Here each of the n streams queues one copy behind a
+// gate kernel (on a stream of its own), so every copy finds the engines before it busy and the
+// n copies start n engines; then the gate opens.  The streams should be the ones the pipeline
+// will use.  Once per process and device for up to the largest n asked for.
+int rt_copy_engines_warm(void* const* streams, int n) {
+    if (!streams || n < 1 || n > 64) return fail(RT_ERR_ARG, "1 to 64 streams");
     int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RT_ERR_NODEV, "no HIP device available");
     HIPCHK(hipGetDevice(&dev));
@@ -3711,12 +3712,13 @@ int rt_copy_engines_warm(void* stream, int n) {
     std::lock_guard<std::mutex> lock(mu);
     if (dev < 0 || dev >= 64 || warmed[dev] >= n) return RT_OK;
     unsigned* flag = nullptr; uint8_t* h = nullptr; uint8_t* d = nullptr;
-    hipStream_t gate = nullptr; hipEvent_t ev = nullptr;
+    hipStream_t gate = nullptr;
+    hipEvent_t ev = nullptr;
     int clk_khz = 0;
-    HIPCHK(hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, dev));
-    HIPCHK(hipHostMalloc((void**)&flag, 4, hipHostMallocCoherent));
     // (copies below the runtime's SDMA threshold run elsewhere: 1 MB each, all into one buffer)
     constexpr size_t B = 1 << 20;
+    HIPCHK(hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeWallClockRate, dev));
+    HIPCHK(hipHostMalloc((void**)&flag, 4, hipHostMallocCoherent));
     HIPCHK(hipHostMalloc((void**)&h, B, hipHostMallocDefault));
     HIPCHK(hipMalloc((void**)&d, B));
     HIPCHK(hipMemset(d, 0, B));
@@ -3729,14 +3731,15 @@ int rt_copy_engines_warm(void* stream, int n) {
     HIPCHK(hipEventRecord(ev, gate));
     hipError_t e = hipSuccess;
     for (int i = 0; i < n && e == hipSuccess; i++) {
-        e = hipStreamWaitEvent((hipStream_t)stream, ev, 0);
-        if (e == hipSuccess) e = hipMemcpyAsync(h, d, B, hipMemcpyDeviceToDeviceNoCU, (hipStream_t)stream);
+        e = hipStreamWaitEvent((hipStream_t)streams[i], ev, 0);
+        if (e == hipSuccess) e = hipMemcpyAsync(h, d, B, hipMemcpyDeviceToDeviceNoCU, (hipStream_t)streams[i]);
     }
     __atomic_store_n(flag, 1u, __ATOMIC_RELEASE);                              // open the gate
     HIPCHK(hipStreamSynchronize(gate));
-    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    for (int i = 0; i < n; i++) HIPCHK(hipStreamSynchronize((hipStream_t)streams[i]));
     HIPCHK(e);
-    (void)hipEventDestroy(ev); (void)hipStreamDestroy(gate);
+    (void)hipEventDestroy(ev);
+    (void)hipStreamDestroy(gate);
     (void)hipFree(d); (void)hipHostFree(h); (void)hipHostFree(flag);
     warmed[dev] = n;
     return RT_OK;

@@ -146,7 +146,7 @@ def lib():
         L.rt_host_alloc.argtypes = [ctypes.c_int64, ctypes.POINTER(vp)]
         L.rt_host_free.argtypes = [vp]
         L.rt_copy_to_host_async.argtypes = [vp, vp, ctypes.c_int64, vp]
-        L.rt_copy_engines_warm.argtypes = [vp, ip]
+        L.rt_copy_engines_warm.argtypes = [ctypes.POINTER(vp), ip]
     _lib = L
     return L
 
@@ -226,9 +226,11 @@ def copy_to_host_async(host_ptr, dev_ptr, nbytes, stream=None):
     _check(lib().rt_copy_to_host_async(host_ptr, dev_ptr, int(nbytes), stream))
 
 
-def copy_engines_warm(stream=None, n=16):
-    """Start n SDMA engines from `stream` ahead of a host-copy pipeline (rt_copy_engines_warm)."""
-    _check(lib().rt_copy_engines_warm(stream, int(n)))
+def copy_engines_warm(streams):
+    """Start the SDMA engines a host-copy pipeline will use: one gated copy from each of
+    `streams` (int hipStream_t handles; rt_copy_engines_warm)."""
+    arr = (ctypes.c_void_p * len(streams))(*streams)
+    _check(lib().rt_copy_engines_warm(arr, len(streams)))
 
 
 def material(Ke=(0, 0, 0, 0), Ka=(0, 0, 0, 0), Kd=(0, 0, 0, 0), Ks=(0, 0, 0, 0), Kt=(0, 0, 0, 0), Kr=(0, 0, 0, 0),

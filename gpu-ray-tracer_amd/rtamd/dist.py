@@ -191,17 +191,24 @@ class FramePipeline:
             self.host_ev = [None] * self.n_host     # D2H copy of the frame last copied into each host buffer
             self.host_no = [-1] * self.n_host       # its frame number
             self.out_copy = [None] * D              # world > 1: the copy that last read each un-permute target
-            # Every host copy on ONE copy stream, after an event of the frame's stream.  The runtime
-            # keeps a stream's copies on the SDMA engine it used last and gives a stream with no
-            # copy history the first idle engine; the first copy on an engine creates its queue
-            # (~7 ms on the host, profiles/r06/rblog/).  Copies from eight render streams spread
-            # over new engines inside the timed window (1.2 ms per frame against 0.67 device-
-            # resident, profiles/r06/rbprobe/); one stream keeps them on one engine.
+            # Host copies are issued once their frame is complete: the host waits for frame k (rank 0
+            # with N > 1: its un-permute) when it issues frame k + lag, then enqueues the copy on the
+            # one copy stream.  A copy enqueued behind a frame still rendering (a stream wait on
+            # the frame's event) waits on the copy engine for that frame's signal, and those waits
+            # measured 0.5-5.6 ms from frame done to copy done for a 0.16-ms copy, a convoy that
+            # held the frames behind it (0.68 ms per frame against 0.59 device-resident); with
+            # the copies issued on completion 0.59-0.61 (profiles/r06/rbprobe/).  lag = depth - 2
+            # keeps depth - 1 frames in flight.
             self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
             self.copy_done = [None] * D             # one rank: the copy that last read parts[s]
-            if self.cuda:                           # the engines the pending copies will spread over
+            self.lag = max(0, D - 2)
+            self.deferred = []                      # (frame, source, ready event, ("part" | "out", slot))
+            if self.cuda:
+                # The runtime gives a copy issued while an earlier one still runs the next idle SDMA
+                # engine, and a copy's first use of an engine creates its queue (~7 ms inside the
+                # enqueue, profiles/r06/rblog/): start the engines these streams will use now.
                 from . import copy_engines_warm
-                copy_engines_warm(self.copy_stream.cuda_stream, 16)
+                copy_engines_warm([self.copy_stream.cuda_stream] + [st.cuda_stream for st in self.streams])
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
         self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
@@ -242,6 +249,33 @@ class FramePipeline:
         self.host_ev[h], self.host_no[h] = ev, k
         return ev
 
+    def _copy_deferred(self):
+        """Issue the oldest deferred host copy (after a host wait for its frame)."""
+        k, src, ev, (kind, s) = self.deferred.pop(0)
+        ev.synchronize()
+        done = self._to_host(k, src, self.copy_stream)
+        if kind == "part":
+            self.copy_done[s] = done
+        else:
+            self.out_copy[s] = done
+
+    def _flush_copies(self, upto=None, key=None):
+        """Issue deferred host copies in frame order: every one up to and including the last that
+        reads `key`; or those of frames <= upto; with neither, all."""
+        if key is not None:
+            n = 1 + max((i for i, e in enumerate(self.deferred) if e[3] == key), default=-1)
+        elif upto is not None:
+            n = sum(1 for e in self.deferred if e[0] <= upto)
+        else:
+            n = len(self.deferred)
+        for _ in range(n):
+            self._copy_deferred()
+
+    def _defer_copy(self, k, src, ready, key):
+        """Frame k's host copy, issued once `ready` (an event after the frame) has completed."""
+        self.deferred.append((k, src, ready, key))
+        self.deferred.sort(key=lambda e: e[0])   # (finish() un-permutes slots out of frame order)
+
     def _unpermute(self, s):
         if not self.pending[s]:
             return
@@ -253,8 +287,10 @@ class FramePipeline:
                 if self.host_staging:           # the gathered host slices -> the slot's device gather buffer
                     g.copy_(self.hgbufs[s])
                 out = self.outs[s % len(self.outs)]
+                if self.readback:
+                    self._flush_copies(key=("out", s))     # frame k - depth's copy has been issued
                 if self.readback and self.out_copy[s] is not None and self.cuda:
-                    self.main.wait_event(self.out_copy[s])  # frame k - depth's copy has read out
+                    self.main.wait_event(self.out_copy[s])  # ... and has read out
                 if self.H % self.world == 0:
                     out.view(self.rows, self.world, self.W).copy_(g.transpose(0, 1))
                 else:
@@ -264,9 +300,7 @@ class FramePipeline:
                 ev = self._event(self.main)
                 self.unperm[s] = ev
                 if self.readback:
-                    if self.cuda:
-                        self.copy_stream.wait_event(ev)
-                    self.out_copy[s] = self._to_host(self.pend_no[s], out, self.copy_stream)
+                    self._defer_copy(self.pend_no[s], out, ev, ("out", s))
 
     def _gather_staged(self):
         """host_staging: issue the gather of the frame staged last (after its staging copy)."""
@@ -301,13 +335,13 @@ class FramePipeline:
         with self._on(st):
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
-            if self.readback and self.world == 1 and self.cuda and self.copy_done[s] is not None:
-                st.wait_event(self.copy_done[s])        # frame k-depth's host copy has read parts[s]
+            if self.readback and self.world == 1:
+                self._flush_copies(key=("part", s))     # frame k-depth's host copy has been issued
+                if self.cuda and self.copy_done[s] is not None:
+                    st.wait_event(self.copy_done[s])    # ... and has read parts[s]
             render(self.parts[s], st)
             if self.readback and self.world == 1:
-                if self.cuda:
-                    self.copy_stream.wait_event(self._event(st))
-                self.copy_done[s] = self._to_host(k, self.parts[s], self.copy_stream)
+                self._defer_copy(k, self.parts[s], self._event(st), ("part", s))
             if self.world > 1:
                 if self.unperm[s] is not None and self.cuda:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]
@@ -317,6 +351,8 @@ class FramePipeline:
                 self.pend_no[s] = k
         if k >= 1:
             self._unpermute((k - 1) % self.depth)
+        if self.readback:
+            self._flush_copies(upto=k - self.lag)
         self.last = k
 
     def host_frame(self, k):
@@ -327,6 +363,7 @@ class FramePipeline:
             self._gather_staged()
         if self.world > 1 and self.pending[s] and self.pend_no[s] == k:
             self._unpermute(s)
+        self._flush_copies(upto=k)
         h = k % self.n_host
         assert self.host_no[h] == k, (k, self.host_no[h])
         self.host_ev[h].synchronize()
@@ -338,6 +375,8 @@ class FramePipeline:
             self._gather_staged()
         for s in range(self.depth):
             self._unpermute(s)
+        if self.readback:
+            self._flush_copies()
         if self.cuda:
             for st in self.streams:
                 self.main.wait_stream(st)

@@ -229,12 +229,13 @@ int rt_host_free(void* p);
  * from rt_host_alloc (pageable memory is staged by the runtime).  Stream-ordered: record an
  * event after it, or synchronize the stream, before reading host_dst. */
 int rt_copy_to_host_async(void* host_dst, const void* dev_src, int64_t bytes, void* stream);
-/* Start n of the device's SDMA copy engines from `stream` (the stream a pipeline's host copies
- * will use), once per process and device.  The runtime hands a copy queued while earlier copies
+/* Start the device's SDMA copy engines a host-copy pipeline will use, once per process and
+ * device: one gated copy from each of the n streams (hipStream_t; the streams the pipeline
+ * copies from or orders copies behind).  The runtime gives a copy queued while earlier copies
  * are still pending the next idle engine, and a copy's first use of an engine creates that
- * engine's queue (~7 ms of host time inside the enqueue): a pipeline with frames in flight would
- * pay that inside its first frames.  Blocks until done; later calls return at once. */
-int rt_copy_engines_warm(void* stream, int n_engines);
+ * engine's queue (~7 ms of host time inside the enqueue): a pipeline with frames in flight
+ * would pay that inside its first timed frames.  Blocks until done. */
+int rt_copy_engines_warm(void* const* streams, int n_streams);
 
 /* Reference-equivalent frame: rebuild BVH if optimize, trace 1 spp, copy the frame into the
  * pinned host canvas on a copy engine, wait for that stream; the framebuffer is host-readable

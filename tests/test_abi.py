@@ -101,8 +101,8 @@ def test_host_copy_entries_without_gpu(rt):
     p = ctypes.c_void_p()
     assert L.rt_host_alloc(0, ctypes.byref(p)) == rt.RT_ERR_ARG
     assert L.rt_host_free(None) == rt.RT_OK
-    assert L.rt_copy_engines_warm(None, 0) == rt.RT_ERR_ARG
+    assert L.rt_copy_engines_warm(None, 1) == rt.RT_ERR_ARG
     if rt.device_count() > 0:
         pytest.skip("a GPU is present")
     assert L.rt_host_alloc(4096, ctypes.byref(p)) == rt.RT_ERR_NODEV
-    assert L.rt_copy_engines_warm(None, 4) == rt.RT_ERR_NODEV
+    assert L.rt_copy_engines_warm((ctypes.c_void_p * 2)(None, None), 2) == rt.RT_ERR_NODEV

@@ -36,6 +36,14 @@ def main():
     torch.cuda.synchronize()
     scene.set_overlap(False, stream=True)
     issue, wait = [], []
+    evs = []
+    if readback:                          # timing events: render done -> copy done, per frame
+        def ev_timed(stream):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            evs.append(e)
+            return e
+        pipe._event = ev_timed
     t0 = time.perf_counter()
     for i in range(n):
         k = 10 + i
@@ -53,8 +61,11 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n * 1e3
     scene.set_overlap(False)
+    lat = [round(evs[2 * i].elapsed_time(evs[2 * i + 1]), 3) for i in range(len(evs) // 2)]
+    gaps = [round(evs[2 * i - 1].elapsed_time(evs[2 * i + 1]), 3) for i in range(1, len(evs) // 2)]
     print(json.dumps({"readback": readback, "ms_per_frame": round(dt, 4),
-                      "issue_ms": [round(x, 3) for x in issue], "wait_ms": [round(x, 3) for x in wait]}), flush=True)
+                      "issue_ms": [round(x, 3) for x in issue], "wait_ms": [round(x, 3) for x in wait],
+                      "render_done_to_copy_done_ms": lat, "copy_done_interval_ms": gaps}), flush=True)
 
 
 if __name__ == "__main__":
