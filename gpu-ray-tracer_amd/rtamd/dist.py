@@ -147,7 +147,10 @@ class FramePipeline:
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
-        self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(D)]
+        # one rank copying frames to the host: twice as many frame buffers as streams, so that a
+        # buffer is rewritten 2 x depth frames after its frame, long after its host copy
+        self.n_parts = 2 * D if (readback and world == 1) else D
+        self.parts = [torch.zeros((self.rows, width), dtype=dtype, device=device) for _ in range(self.n_parts)]
         # CPU tensors (the gloo tests of the multi-process logic): no streams, no events
         self.cuda = str(device).startswith("cuda")
         # streams: the render streams to reuse (at least `depth` of them; e.g. a later pipeline in
@@ -200,8 +203,11 @@ class FramePipeline:
             # the copies issued on completion 0.59-0.61 (profiles/r06/rbprobe/).  lag = depth - 2
             # keeps depth - 1 frames in flight.
             self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
-            self.copy_done = [None] * D             # one rank: the copy that last read parts[s]
-            self.lag = max(0, D - 2)
+            self.copy_done = [None] * self.n_parts  # one rank: the copy that last read parts[p]
+            # copies trail the frames issued by `lag`: the host waits for frame k - lag as it issues
+            # frame k, so lag + 1 frames stay in flight (one rank: depth, as device-resident frames;
+            # N > 1: depth - 1, the un-permute targets are reused after depth frames)
+            self.lag = max(0, D - 1) if world == 1 else max(0, D - 2)
             self.deferred = []                      # (frame, source, ready event, ("part" | "out", slot))
             if self.cuda:
                 # The runtime gives a copy issued while an earlier one still runs the next idle SDMA
@@ -229,7 +235,7 @@ class FramePipeline:
     def frame(self):
         """The last finished frame (rank 0; call finish() first)."""
         if self.world == 1:
-            return self.parts[self.last % self.depth] if self.last >= 0 else None
+            return self.parts[self.last % self.n_parts] if self.last >= 0 else None
         return self.out
 
     def _to_host(self, k, src, stream):
@@ -335,13 +341,14 @@ class FramePipeline:
         with self._on(st):
             if self.work[s] is not None:
                 self.work[s].wait()                     # frame k-depth's gather has read parts[s]
+            p = k % self.n_parts
             if self.readback and self.world == 1:
-                self._flush_copies(key=("part", s))     # frame k-depth's host copy has been issued
-                if self.cuda and self.copy_done[s] is not None:
-                    st.wait_event(self.copy_done[s])    # ... and has read parts[s]
-            render(self.parts[s], st)
+                self._flush_copies(key=("part", p))     # frame k - 2 depth's host copy has been issued
+                if self.cuda and self.copy_done[p] is not None:
+                    st.wait_event(self.copy_done[p])    # ... and has read parts[p]
+            render(self.parts[p], st)
             if self.readback and self.world == 1:
-                self._defer_copy(k, self.parts[s], self._event(st), ("part", s))
+                self._defer_copy(k, self.parts[p], self._event(st), ("part", p))
             if self.world > 1:
                 if self.unperm[s] is not None and self.cuda:
                     st.wait_event(self.unperm[s])       # frame k-depth's un-permute has read gbufs[s]

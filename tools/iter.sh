@@ -16,6 +16,6 @@ for i in 1 2; do
   timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline "$@" > $O/bench20_$i.log 2>&1 || { echo "bench failed"; tail -30 $O/bench20_$i.log; exit 1; }
   tail -1 $O/bench20_$i.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('bench', d['ms_per_step'], d['value'], 'dev', d.get('device_resident'), 'cold', d.get('cold_frame_ms'), 'load', d.get('scene_load_ms'), 'lat', d.get('frame_latency_ms'), 'cam', (d.get('camera_path') or {}).get('ms_per_step'))"
 done
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$R/$O/kt20" -o kt20 -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-camera-path "$@" > "$R/$O/kt20.log" 2>&1) || { echo "kt20 failed"; tail "$R/$O/kt20.log"; exit 1; }
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/kt20" -o kt20 -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-camera-path "$@" > "$R/$O/kt20.log" 2>&1) || { echo "kt20 failed"; tail "$R/$O/kt20.log"; exit 1; }
 cut -c1-150 $O/kt20/kt20_kernel_stats.csv
 echo "iter done"

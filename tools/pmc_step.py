@@ -108,8 +108,7 @@ def main():
                 entry["window"] = {
                     "grid_timed_frames": d.get("config", {}).get("grid_timed_frames"),
                     "frames_in_flight": d.get("frames_in_flight"),
-                    "timed_to": ("host" if str(d.get("timed_to", "")).startswith("host") else "device")
-                                if d.get("frames_in_flight", 1) > 1 else "serial",
+                    "timed_to": d.get("pmc_window", "device") if d.get("frames_in_flight", 1) > 1 else "serial",
                     "lib_sha16": d.get("build", {}).get("lib_sha16")}
     if b:
         entry["gpu_busy_ms_per_step"] = b["busy_ns"] / steps / 1e6

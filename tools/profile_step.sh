@@ -13,7 +13,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
 STEPS=${STEPS:-20}
-ARGS="--steps $STEPS --warmup 5 --no-cpu-baseline --no-camera-path $*"
+ARGS="--steps $STEPS --warmup 5 --no-cpu-baseline --no-camera-path --pmc-window device $*"
 run() { local name=$1; shift; timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o "$name" -- python3 "$R/bench.py" $ARGS > "$OUT/$name.log" 2>&1; }
 run kt --kernel-trace --stats || { echo "kernel-trace run failed"; exit 1; }
 run fetch --kernel-trace --pmc FETCH_SIZE || { echo "pmc FETCH_SIZE failed"; exit 1; }
