@@ -170,16 +170,30 @@ int main(int argc, char** argv) {
         delete scene;
         return 0;
     }
+    // spp > 1 / textures (build extensions): the frame as update_scene leaves it -- rendered into a
+    // device buffer, copied by a copy engine into pinned host memory, waited for -- with the
+    // buffers made before any timing, as the reference's canvas is made with the scene
+    uint32_t* dframe = nullptr;
+    uint32_t* hframe = nullptr;
+    hipStream_t dst = nullptr;
+    if (spp != 1 || textures) {
+        void* hp = nullptr;
+        if (hipMalloc((void**)&dframe, (size_t)W * H * 4) != hipSuccess ||
+            hipStreamCreateWithFlags(&dst, hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP allocation failed\n"); return 1; }
+        rtamd_detail::check(rt_host_alloc((int64_t)W * H * 4, &hp), "rt_host_alloc");
+        hframe = static_cast<uint32_t*>(hp);
+    }
     auto draw = [&]() {
         if (spp == 1 && !textures) {
             rtracer::gpu::update_scene(scene, dim, !unopt);
         } else {
-            host.resize((size_t)W * H);
             rt_render_opts o;
             rt_render_opts_default(&o);
             o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
-            o.rgba = host.data(); o.host_outputs = 1;
+            o.rgba = dframe; o.stream = dst; o.sync = 0;
             rtamd_detail::check(rt_render(scene->handle(), &o, nullptr), "rt_render");
+            rtamd_detail::check(rt_copy_to_host_async(hframe, dframe, (int64_t)W * H * 4, dst), "rt_copy_to_host_async");
+            if (hipStreamSynchronize(dst) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); std::exit(1); }
         }
     };
     if (bench) {
@@ -198,9 +212,10 @@ int main(int argc, char** argv) {
         rtracer::gpu::debug_cast(scene, dbg_x, dbg_y);
     }
     if (!out.empty()) {
-        const uint32_t* px = (spp == 1 && !textures) ? env.get_canvas().get_buffer() : host.data();
+        const uint32_t* px = (spp == 1 && !textures) ? env.get_canvas().get_buffer() : hframe;
         if (!px || !write_ppm(out.c_str(), px, W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
     }
+    if (dframe) { (void)hipStreamDestroy(dst); (void)hipFree(dframe); (void)rt_host_free(hframe); }
     renv::gpu::Scene::free(*scene);
     delete scene;
     return 0;

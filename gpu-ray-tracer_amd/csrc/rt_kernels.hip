@@ -4221,10 +4221,9 @@ static int warm_scene(rt_scene* s) {
     int n = 0;
     if (off || hipGetDeviceCount(&n) != hipSuccess || n <= 0) { (void)hipGetLastError(); return RT_OK; }
     const std::string saved = g_err;
-    rt_render_opts o;
-    rt_render_opts_default(&o);
-    o.sync = 1;
-    if (s->h.cam.W > 0 && s->h.cam.H > 0 && rt_render(s, &o, nullptr) != RT_OK) {
+    // update_scene's own path: a 1-spp frame and its copy into the pinned canvas (the copy starts
+    // the copy engine's queue for device-to-host transfers, ~7 ms the first time)
+    if (s->h.cam.W > 0 && s->h.cam.H > 0 && rt_update_scene(s, 16, 1) != RT_OK) {
         g_err = saved;                                    // left for the caller's first render to report
         (void)hipGetLastError();
     }
