@@ -2927,6 +2927,40 @@ int ensure_history(rt_scene* s, int n_groups, const long long* key, hipStream_t 
     return RT_OK;
 }
 
+// Per-frame buffers (sky flags, live lists, scheduling history) sized for a layout of n_groups
+// pixel groups in the current slot and every allocated one, ahead of the first frame that needs
+// them (warm_scene: the whole frame at 2-8 pixels per wave, the layouts of spp 8-32).  Contents
+// are reset at first use as before (the history key); only capacity is reserved here.
+int reserve_layout(rt_scene* s, int n_groups) {
+    const int cap = (std::max(n_groups, 1024) + 3) & ~3;
+    bool grew = false;
+    if (cap > s->gsky_cap) {
+        dfree(s->d_gsky);
+        HIPCHK(hipMalloc((void**)&s->d_gsky, cap));
+        s->gsky_cap = cap; grew = true;
+    }
+    const int sblocks = (n_groups + 63) / 64;
+    const int need = (sblocks + NQ - 1) / NQ * 64 * NQ + n_groups;
+    if (need > s->live_cap) {
+        dfree(s->d_live);
+        HIPCHK(hipMalloc((void**)&s->d_live, (size_t)need * sizeof(int)));
+        s->live_cap = need; grew = true;
+    }
+    if (cap > s->hist_cap) {
+        for (int p = 0; p < 2; p++) { dfree(s->d_hlist[p]); dfree(s->d_hflag[p]); }
+        dfree(s->d_hctl);
+        for (int p = 0; p < 2; p++) {
+            HIPCHK(hipMalloc((void**)&s->d_hlist[p], cap * sizeof(int)));
+            HIPCHK(hipMalloc((void**)&s->d_hflag[p], cap));
+        }
+        HIPCHK(hipMalloc((void**)&s->d_hctl, 4 * sizeof(unsigned long long)));
+        s->hist_cap = cap;
+        s->hist_key[0] = -1;
+        grew = true;
+    }
+    return (grew && s->n_slots > 1) ? mirror_slot_caps(s) : RT_OK;
+}
+
 int ensure_spp(rt_scene* s, int spp) {
     if (spp <= s->spp_cap) return RT_OK;
     int cap = std::max(spp, 64);
@@ -4226,7 +4260,11 @@ static int warm_scene(rt_scene* s) {
     if (s->h.cam.W > 0 && s->h.cam.H > 0 && rt_update_scene(s, 16, 1) != RT_OK) {
         g_err = saved;                                    // left for the caller's first render to report
         (void)hipGetLastError();
+        return RT_OK;
     }
+    // capacity for the whole frame at 8 pixels per wave (4 x 2 groups: 8-32 spp, the bench's layout)
+    const long long groups = (long long)((s->h.cam.W + 3) / 4) * ((s->h.cam.H + 1) / 2);
+    if (groups < (1ll << 26) && reserve_layout(s, (int)groups) != RT_OK) { g_err = saved; (void)hipGetLastError(); }
     return RT_OK;
 }
 
