@@ -9,12 +9,12 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do LIBS+=("$1"); shift; done
 [ "$1" == "--" ] && shift
 for r in $(seq 1 $ROUNDS); do
   for L in "${LIBS[@]}"; do
-    RTAMD_LIB=$L timeout -k 10 120 python3 "$R/bench.py" --no-cpu-baseline --steps 20 --warmup 3 "$@" > /tmp/ab_out.txt 2>&1 || { cat /tmp/ab_out.txt; exit 1; }
+    RTAMD_LIB=$L timeout -k 10 120 python3 "$R/bench.py" --no-cpu-baseline --steps ${AB_STEPS:-20} --warmup 3 --no-camera-path "$@" > /tmp/ab_out.txt 2>&1 || { cat /tmp/ab_out.txt; exit 1; }
     python3 - "$L" <<'PY'
 import json, sys
 line = [l for l in open('/tmp/ab_out.txt') if l.startswith('{')][-1]
 d = json.loads(line)
-print("%-40s frame %.4f ms  trace %.4f ms  bvh %.4f  %.1f Mrays/s" % (sys.argv[1].split('/')[-1], d['ms_per_step'], d['trace_kernel_ms'], d['bvh_build_ms'], d['value']))
+print("%-40s frame %.4f ms  device-resident %.4f  trace %.4f ms  bvh %.4f  %.1f Mrays/s" % (sys.argv[1].split('/')[-1], d['ms_per_step'], (d.get('device_resident') or {}).get('ms_per_step', float('nan')), d['trace_kernel_ms'], d['bvh_build_ms'], d['value']))
 PY
   done
 done
