@@ -11,6 +11,9 @@ cd "$R" || exit 1
 F=${FINAL:-r06/final}
 O=gpurun_out/$F
 mkdir -p $O
+# PART=a: suite, smoke, benches, per-step PMC, kernel trace, headline PMC; PART=b: config 5 PMC,
+# the other configs, CLI -b, the copy check (two gpurun calls of < 20 min each); default both
+if [ "${PART:-ab}" != "b" ]; then
 timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
@@ -22,6 +25,8 @@ for f in bench20_1 bench20_2 bench60; do tail -1 $O/$f.log | python3 -c "import 
 timeout -k 10 600 bash tools/profile_step.sh $F/step_w8s > $O/profile_step.log 2>&1 || { echo "profile_step failed"; tail $O/profile_step.log; exit 1; }
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/kt20" -o kt20 -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-camera-path > "$R/$O/kt20.log" 2>&1) || { echo "kt20 failed"; exit 1; }
 timeout -k 10 900 bash tools/profile.sh $F/prof_w8s > $O/profile.log 2>&1 || { echo "profile failed"; tail $O/profile.log; exit 1; }
+fi
+[ "${PART:-ab}" == "a" ] && { echo "part a done"; exit 0; }
 QUICK=1 timeout -k 10 400 bash tools/profile.sh $F/prof_w16 --scene world16 --width 3840 --height 2160 --spp 64 > $O/prof_w16.log 2>&1 || { echo "profile w16 failed"; tail $O/prof_w16.log; exit 1; }
 W16="--scene world16 --width 3840 --height 2160 --spp 64 --steps 6 --warmup 2 --no-cpu-baseline --no-camera-path"
 timeout -k 10 300 python3 -u bench.py $W16 > $O/cfg_world16.log 2>&1 || { echo "w16 failed"; exit 1; }
