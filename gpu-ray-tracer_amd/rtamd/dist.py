@@ -277,6 +277,9 @@ class FramePipeline:
         for _ in range(n):
             self._copy_deferred()
 
+    def _done(self, ev):
+        return ev.query() if self.cuda else True
+
     def _defer_copy(self, k, src, ready, key):
         """Frame k's host copy, issued once `ready` (an event after the frame) has completed."""
         self.deferred.append((k, src, ready, key))
@@ -360,6 +363,10 @@ class FramePipeline:
             self._unpermute((k - 1) % self.depth)
         if self.readback:
             self._flush_copies(upto=k - self.lag)
+            # and every copy whose frame has already completed (no wait): a copy starts as soon as
+            # the host sees its frame done, so the window's last frames leave few copies behind
+            while self.deferred and self._done(self.deferred[0][2]):
+                self._copy_deferred()
         self.last = k
 
     def host_frame(self, k):

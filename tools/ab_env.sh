@@ -10,8 +10,8 @@ mkdir -p "$OUT"
 for i in $(seq 1 "$ROUNDS"); do
   for arm in "$@"; do
     n=$(echo "$arm" | tr -c 'A-Za-z0-9_\n' '_')
-    env $arm timeout -k 10 240 python3 -u "$R/bench.py" --steps ${STEPS:-60} --warmup 5 --no-cpu-baseline \
+    env $arm timeout -k 10 240 python3 -u "$R/bench.py" --steps ${STEPS:-60} --warmup 5 --no-cpu-baseline --no-camera-path \
       > "$OUT/bench_${n}_$i.log" 2>&1 || { echo "bench $arm round $i failed"; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%-24s round %s frame_ms %.4f trace %.4f latency %.4f readback %.4f' % (sys.argv[2], sys.argv[3], d['frame_ms'], d['trace_kernel_ms'], d['frame_latency_ms'], d['ms_per_step_with_readback']))" "$OUT/bench_${n}_$i.log" "$arm" $i
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('%-24s round %s frame_ms %.4f device-resident %.4f trace %.4f latency %.4f cold %.4f' % (sys.argv[2], sys.argv[3], d['frame_ms'], (d.get('device_resident') or {}).get('ms_per_step', float('nan')), d['trace_kernel_ms'], d['frame_latency_ms'], d.get('cold_frame_ms', float('nan'))))" "$OUT/bench_${n}_$i.log" "$arm" $i
   done
 done
