@@ -32,7 +32,7 @@ static void usage() {
     std::fprintf(stderr,
                  "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
                  "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]] [--gpus N [--ranks R]]\n"
-                 "               [--in-flight D]\n");
+                 "               [--in-flight D [--readback]]\n");
 }
 
 static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
@@ -53,7 +53,7 @@ static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
 
 int main(int argc, char** argv) {
     std::string config, out;
-    bool bench = false, unopt = false, serial = false, textures = false;
+    bool bench = false, unopt = false, serial = false, textures = false, readback = false;
     std::string atlas;
     int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1, gpus = 1, ranks = 0, in_flight = 0;
     for (int i = 1; i < argc; i++) {
@@ -75,6 +75,7 @@ int main(int argc, char** argv) {
         else if (a == "--gpus") gpus = std::atoi(val("--gpus"));
         else if (a == "--ranks") ranks = std::atoi(val("--ranks"));
         else if (a == "--in-flight") in_flight = std::atoi(val("--in-flight"));
+        else if (a == "--readback") readback = true;
         else if (a == "--textures") {
             textures = true;
             if (i + 1 < argc && argv[i + 1][0] != '-') atlas = argv[++i];
@@ -125,23 +126,68 @@ int main(int argc, char** argv) {
         const int D = in_flight;
         const bool split = gpus > 1 || ranks > 1;
         rtamd_detail::check(rt_scene_set_frame_slots(handle, D), "rt_scene_set_frame_slots");
+        // --readback (the reference's post-condition for every frame, main.cc's loop blits each
+        // canvas): each frame is copied into pinned host memory by a copy engine once it is
+        // complete -- the host waits for frame f - (D - 1) as it issues frame f and copies it then,
+        // and copies any frame it sees complete -- on one copy stream; frame
+        // buffers are 2 D deep so a buffer is rewritten long after its copy.  Single device.
+        const bool rb = readback && !split;
+        const int NB = rb ? 2 * D : D;
         std::vector<hipStream_t> st(D);
-        std::vector<uint32_t*> buf(D);
-        for (int k = 0; k < D; k++) {
-            if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
-                hipMalloc((void**)&buf[k], (size_t)W * H * 4) != hipSuccess) { std::fprintf(stderr, "HIP allocation failed\n"); return 1; }
+        std::vector<uint32_t*> buf(NB);
+        std::vector<uint32_t*> hbuf(rb ? NB : 0);
+        std::vector<hipEvent_t> ev_done(NB), ev_copy(NB);
+        std::vector<char> copied(NB, 0);
+        hipStream_t cst = nullptr;
+        for (int k = 0; k < D; k++)
+            if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); return 1; }
+        for (int k = 0; k < NB; k++) {
+            if (hipMalloc((void**)&buf[k], (size_t)W * H * 4) != hipSuccess) { std::fprintf(stderr, "HIP allocation failed\n"); return 1; }
+            if (rb) {
+                void* hp = nullptr;
+                rtamd_detail::check(rt_host_alloc((int64_t)W * H * 4, &hp), "rt_host_alloc");
+                hbuf[k] = static_cast<uint32_t*>(hp);
+                if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&ev_copy[k], hipEventDisableTiming) != hipSuccess) { std::fprintf(stderr, "HIP event failed\n"); return 1; }
+            }
         }
-        long long f = 0;
+        if (rb) {
+            if (hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); return 1; }
+            std::vector<void*> ws{cst};
+            for (auto x : st) ws.push_back(x);
+            rtamd_detail::check(rt_copy_engines_warm(ws.data(), (int)ws.size()), "rt_copy_engines_warm");
+        }
+        long long f = 0, next_copy = 0;                        // frames [next_copy, f) await their copies
+        const long long lag = D > 1 ? D - 1 : 0;
+        auto copy_frame = [&](bool wait) -> bool {             // the oldest uncopied frame, if complete
+            const int b = (int)(next_copy % NB);
+            if (wait) { if (hipEventSynchronize(ev_done[b]) != hipSuccess) std::exit(1); }
+            else if (hipEventQuery(ev_done[b]) != hipSuccess) return false;
+            rtamd_detail::check(rt_copy_to_host_async(hbuf[b], buf[b], (int64_t)W * H * 4, cst), "rt_copy_to_host_async");
+            if (hipEventRecord(ev_copy[b], cst) != hipSuccess) std::exit(1);
+            copied[b] = 1;
+            next_copy++;
+            return true;
+        };
         auto issue = [&]() {
+            const int b = (int)(f % NB);
             rt_render_opts o;
             rt_render_opts_default(&o);
             o.spp = spp; o.use_bvh = unopt ? 0 : 1; o.kernel_dim = dim; o.textures = textures ? 1 : 0;
-            o.rgba = buf[f % D]; o.sync = 0;                  // asynchronous: frames overlap
+            o.rgba = buf[b]; o.sync = 0;                       // asynchronous: frames overlap
             // single device: frame f on stream f % D.  Split frames (use_devices) run on the
             // library's per-slot streams; a caller stream would only add event waits, which block
             // whatever else HIP mapped onto that stream's hardware queue
             o.stream = split ? nullptr : st[f % D];
+            if (rb && copied[b] && hipStreamWaitEvent(st[f % D], ev_copy[b], 0) != hipSuccess) std::exit(1);
             rtamd_detail::check(rt_render(handle, &o, nullptr), "rt_render");
+            if (rb) {
+                if (hipEventRecord(ev_done[b], st[f % D]) != hipSuccess) std::exit(1);
+                f++;
+                while (next_copy < f - lag) copy_frame(true);
+                while (next_copy < f && copy_frame(false)) {}
+                return;
+            }
             f++;
         };
         auto wait_all = [&]() {
@@ -149,6 +195,10 @@ int main(int argc, char** argv) {
                 for (int d = gpus - 1; d >= 0; d--) { (void)hipSetDevice(d); (void)hipDeviceSynchronize(); }
             }
             else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
+            if (rb) {
+                while (next_copy < f) copy_frame(true);
+                (void)hipStreamSynchronize(cst);               // every frame is on the host
+            }
         };
         for (int k = 0; k < 2 * D; k++) issue();          // warm-up: slots, streams, scheduling history
         wait_all();
@@ -158,14 +208,24 @@ int main(int argc, char** argv) {
         auto to = std::chrono::high_resolution_clock::now();
         const double ms = std::chrono::duration<double, std::milli>(to - from).count() / frames;
         const int slices = (gpus > 1 || ranks > 1) ? (ranks > 0 ? ranks : gpus) : 1;
-        std::printf("In flight %d: %.4f ms/frame, %.4f ms per slice (%d slices on %d GPU(s), %d frames)\n", D, ms,
-                    ms * gpus / slices, slices, gpus, frames);
+        std::printf("In flight %d%s: %.4f ms/frame, %.4f ms per slice (%d slices on %d GPU(s), %d frames)\n", D,
+                    rb ? " (host-readable)" : "", ms, ms * gpus / slices, slices, gpus, frames);
         if (!out.empty()) {
-            host.resize((size_t)W * H);
-            if (hipMemcpy(host.data(), buf[(f - 1) % D], host.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-                !write_ppm(out.c_str(), host.data(), W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
+            const uint32_t* px = nullptr;
+            if (rb) px = hbuf[(f - 1) % NB];
+            else {
+                host.resize((size_t)W * H);
+                if (hipMemcpy(host.data(), buf[(f - 1) % NB], host.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) px = nullptr;
+                else px = host.data();
+            }
+            if (!px || !write_ppm(out.c_str(), px, W, H)) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 1; }
         }
-        for (int k = 0; k < D; k++) { (void)hipStreamDestroy(st[k]); (void)hipFree(buf[k]); }
+        for (int k = 0; k < D; k++) (void)hipStreamDestroy(st[k]);
+        for (int k = 0; k < NB; k++) {
+            (void)hipFree(buf[k]);
+            if (rb) { (void)rt_host_free(hbuf[k]); (void)hipEventDestroy(ev_done[k]); (void)hipEventDestroy(ev_copy[k]); }
+        }
+        if (cst) (void)hipStreamDestroy(cst);
         renv::gpu::Scene::free(*scene);
         delete scene;
         return 0;

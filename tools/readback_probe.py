@@ -19,12 +19,17 @@ import rtamd.dist as rtdist  # noqa: E402
 
 def main():
     readback = (sys.argv[1] if len(sys.argv) > 1 else "1") == "1"
+    scene_name = sys.argv[2] if len(sys.argv) > 2 else "world8_stress"
+    clamp = int(os.environ.get("RT_PROBE_COPY_BYTES", "0"))
+    if clamp:                             # experiment: copies cut to `clamp` bytes (sync cost vs data)
+        real = rtamd.copy_to_host_async
+        rtamd.copy_to_host_async = lambda h, d, n, st=None: real(h, d, min(n, clamp), st)
     n = 40
     W, H, D = 1920, 1080, 8
     pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", None, depth=D, readback=readback)
     for st in pipe.streams + ([pipe.copy_stream] if readback else []):
         torch.cuda.Event().record(st)
-    scene = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", "world8_stress.json"), W, H)
+    scene = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", scene_name + ".json"), W, H)
     scene.set_frame_slots(D)
     torch.cuda.synchronize()
 
