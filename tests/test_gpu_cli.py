@@ -154,11 +154,13 @@ def test_cpp_shim_main_cc_calls(oracle, tmp_path):
     assert (frame != 0).any()
 
 
-@pytest.mark.parametrize("extra", [["--in-flight", "4"], ["--gpus", "1", "--ranks", "8", "--in-flight", "8"]])
+@pytest.mark.parametrize("extra", [["--in-flight", "4"], ["--gpus", "1", "--ranks", "8", "--in-flight", "8"],
+                                   ["--in-flight", "8", "--readback"], ["--in-flight", "3", "--readback"]])
 def test_cli_frames_in_flight(oracle, tmp_path, extra):
     """--in-flight D: frames issued asynchronously, D in flight, each into its own device buffer on
     its own stream (single device, and 8 row-cyclic slices through rt_scene_set_devices with one
-    slot's streams per frame); the last frame equals the oracle's."""
+    slot's streams per frame); --readback: every frame copied to pinned host memory by a copy
+    engine once complete (the written frame is the host copy); the last frame equals the oracle's."""
     out = str(tmp_path / "p.ppm")
     r = subprocess.run([CLI, "-c", scene_path("world8_stress"), "--width", "240", "--height", "136", "--spp", "2",
                         "--frames", "12", "--out", out] + extra, capture_output=True, text=True, timeout=120,
