@@ -21,6 +21,7 @@ def main():
     readback = (sys.argv[1] if len(sys.argv) > 1 else "1") == "1"
     scene_name = sys.argv[2] if len(sys.argv) > 2 else "world8_stress"
     clamp = int(os.environ.get("RT_PROBE_COPY_BYTES", "0"))
+    no_consumer = os.environ.get("RT_PROBE_NO_CONSUMER", "0") == "1"   # experiment: no per-frame host read
     if clamp:                             # experiment: copies cut to `clamp` bytes (sync cost vs data)
         real = rtamd.copy_to_host_async
         rtamd.copy_to_host_async = lambda h, d, n, st=None: real(h, d, min(n, clamp), st)
@@ -55,7 +56,7 @@ def main():
         a = time.perf_counter()
         pipe.step(k, render)
         b = time.perf_counter()
-        if readback and k - pipe.n_host + 1 >= 10:
+        if readback and k - pipe.n_host + 1 >= 10 and not no_consumer:
             pipe.host_frame(k - pipe.n_host + 1)
         c = time.perf_counter()
         issue.append((b - a) * 1e3)
