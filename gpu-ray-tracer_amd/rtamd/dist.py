@@ -125,8 +125,8 @@ class FramePipeline:
     host-readable, raytracer.cu:102-120 / canvas.cu:23-29) without giving up the overlap: the
     finished frame (rank 0) is copied into pinned host buffer k % host_buffers (rt_host_alloc)
     by a copy-engine transfer (rt_copy_to_host_async: no blit kernel, no CU taken from the
-    frames in flight) -- on the render stream for one rank, on a copy stream after the
-    un-permute otherwise -- while later frames render.  `host_frame(k)` waits for frame k's
+    frames in flight), issued on one copy stream once the frame (N > 1: its un-permute) has
+    completed, while later frames render (see the comment in __init__).  `host_frame(k)` waits for frame k's
     copy; a host buffer is reused host_buffers frames later, after its copy (and the caller's
     read) is done, so a consumer may read frames up to host_buffers - 1 behind the last one
     issued.  host_buffers defaults to 2 x depth: the frames the consumer has not read yet are
@@ -200,8 +200,7 @@ class FramePipeline:
             # the frame's event) waits on the copy engine for that frame's signal, and those waits
             # measured 0.5-5.6 ms from frame done to copy done for a 0.16-ms copy, a convoy that
             # held the frames behind it (0.68 ms per frame against 0.59 device-resident); with
-            # the copies issued on completion 0.59-0.61 (profiles/r06/rbprobe/).  lag = depth - 2
-            # keeps depth - 1 frames in flight.
+            # the copies issued on completion 0.59-0.61 (profiles/r06/rbprobe/).
             self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
             self.copy_done = [None] * self.n_parts  # one rank: the copy that last read parts[p]
             # copies trail the frames issued by `lag`: the host waits for frame k - lag as it issues
