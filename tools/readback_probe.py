@@ -28,6 +28,18 @@ def main():
     n = 40
     W, H, D = 1920, 1080, 8
     pipe = rtdist.FramePipeline(W, H, 1, 0, "cuda", None, depth=D, readback=readback)
+    if os.environ.get("RT_PROBE_HIPMALLOC", "0") == "1":     # experiment: frame buffers from hipMalloc
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+
+        class Dev:
+            def __init__(self, n):
+                self.p = ctypes.c_void_p()
+                assert hip.hipMalloc(ctypes.byref(self.p), ctypes.c_size_t(n * 4)) == 0
+                self.__cuda_array_interface__ = {"shape": (H, W), "typestr": "<i4", "data": (self.p.value, False),
+                                                 "version": 2}
+        pipe._devbufs = [Dev(W * H) for _ in pipe.parts]
+        pipe.parts = [torch.as_tensor(b, device="cuda") for b in pipe._devbufs]
     for st in pipe.streams + ([pipe.copy_stream] if readback else []):
         torch.cuda.Event().record(st)
     scene = rtamd.Scene.load_json(os.path.join(ROOT, "scenes", scene_name + ".json"), W, H)
