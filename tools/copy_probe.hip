@@ -47,6 +47,29 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%s: %zu B, %.4f ms per copy, %.1f GB/s\n", mode, n, ms / 40, n / (ms / 40 * 1e-3) / 1e9);
+    // the same bytes as two halves on two streams at once (two copy engines)
+    {
+        hipStream_t c2; CK(hipStreamCreateWithFlags(&c2, hipStreamNonBlocking));
+        hipEvent_t f0, f1; CK(hipEventCreate(&f0)); CK(hipEventCreate(&f1));
+        const size_t h2 = (n / 2) & ~(size_t)255;
+        for (int w = 0; w < 2; w++) {                                      // w = 0: warm both engines
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, a));
+            CK(hipStreamWaitEvent(c2, e0, 0));
+            for (int i = 0; i < 40; i++) {
+                CK(hipMemcpyAsync(h, d, h2, kind, a));
+                CK(hipMemcpyAsync((char*)h + h2, (const char*)d + h2, n - h2, kind, c2));
+            }
+            CK(hipEventRecord(f0, c2));
+            CK(hipStreamWaitEvent(a, f0, 0));
+            CK(hipEventRecord(e1, a));
+            CK(hipStreamSynchronize(a));
+        }
+        float m2 = 0;
+        CK(hipEventElapsedTime(&m2, e0, e1));
+        if (memcmp(h, src.data(), n)) { printf("%s split: DATA MISMATCH\n", mode); return 2; }
+        printf("%s split over two streams: %.4f ms per frame, %.1f GB/s\n", mode, m2 / 40, n / (m2 / 40 * 1e-3) / 1e9);
+    }
     int dev = 0, freq = 0, ncu = 0;
     CK(hipGetDevice(&dev));
     CK(hipDeviceGetAttribute(&freq, hipDeviceAttributeWallClockRate, dev));     // kHz
