@@ -6,16 +6,17 @@ Metric (BASELINE.json): Mrays/s (primary + secondary, i.e. every closest-hit que
 1920x1080, 8 spp, BVH, on N MI355X.
 
 One step = one frame: per-frame BVH rebuild + the trace kernel over this rank's
-rows (row-cyclic: y = rank, rank+N, ...) into HBM, then (N > 1) an RCCL gather of
-the packed RGBA8 rows to rank 0 and the row un-permute.  Frames are pipelined eight deep
-(rtamd.dist.FramePipeline, rt_scene_set_frame_slots): frame k+1 renders on another
-stream and starts on the CUs that the previous frames' longest pixel groups leave idle,
-and frame k's gather runs on the collective stream meanwhile.  The timed region ends after the last
-frame's gather and un-permute.  `frame_latency_ms` is one frame issued alone and waited
-for; `--no-overlap` times serial frames.  The frame stays in HBM for `value`; the reference's
-post-condition (frame host-readable when update_scene returns) is timed separately as
-`ms_per_step_with_readback`: the same pipeline with each finished frame copied to pinned host
-memory asynchronously while later frames render (FramePipeline(readback=True)).
+rows (row-cyclic: y = rank, rank+N, ...), then (N > 1) an RCCL gather of the packed RGBA8
+rows to rank 0 and the row un-permute, then the frame's copy into pinned host memory on a
+DMA copy engine (rank 0), read by a host consumer: the reference's post-condition, the frame
+host-readable when update_scene returns (raytracer.cu:102-120).  Frames are pipelined eight
+deep (rtamd.dist.FramePipeline(readback=True), rt_scene_set_frame_slots): frame k+1 renders on
+another stream and starts on the CUs that the previous frames' longest pixel groups leave idle,
+frame k's gather runs on the collective stream meanwhile, and each host copy is issued once its
+frame has completed.  The timed region ends when the last frame is on the host.
+The same frames left in HBM are timed afterwards as `device_resident`; `frame_latency_ms` is
+one host-readable frame issued alone and waited for, `cold_frame_ms` the first one after the
+scene is loaded; `--no-overlap` times serial frames.
 
 Units.  `value` counts rays in the reference's units (every cast_ray call of
 propagate_ray, taken from a counted render of the same frame): reference-equivalent rays.
