@@ -455,6 +455,26 @@ def main():
         lat.append(time.perf_counter() - t3)
     lat_ms = sorted(lat)[len(lat) // 2] * 1e3
     tm = scene.timing_collect()
+    # this box's copy-engine rate for one full frame to pinned host memory, alone (rank 0; the
+    # rate is a property of the box at the time of the call -- 29 or 53 GB/s seen)
+    copy_rate = None
+    if overlap and rank == 0 and fbr is not None and fbr.copy_stream is not None:
+        src = torch.zeros((H, W), dtype=torch.int32, device="cuda")
+        hb = rtamd.HostBuffer((H, W), "int32")
+        cs = fbr.copy_stream
+        cs.wait_stream(torch.cuda.current_stream())
+        for rep in range(2):
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(cs)
+            for _ in range(20):
+                rtamd.copy_to_host_async(hb.ptr, src.data_ptr(), 4 * W * H, cs.cuda_stream)
+            c1.record(cs)
+            cs.synchronize()
+        cms = c0.elapsed_time(c1) / 20
+        copy_rate = {"frame_copy_ms": round(cms, 4), "GBs": round(4 * W * H / (cms * 1e-3) / 1e9, 1),
+                     "source": "20 back-to-back frame copies on the copy stream, event-timed, after the timed windows"}
+        hb.free()
+        del src
     # Moving camera (the reference's real caller moves it every frame, main.cc:140-180): the
     # same K host-readable frames with main.cc's key and mouse steps applied before each, so the
     # previous frame's heavy-group flags (history-driven scheduling) are one pose stale.
@@ -588,6 +608,8 @@ def main():
         out["device_resident"] = {
             "ms_per_step": round(dev_s / args.steps * 1e3, 4), "value": round(rays * args.steps / dev_s / 1e6, 3),
             "unit": "Mrays/s", "note": "the same K frames left in HBM (no host copy), measured after the headline"}
+    if copy_rate:
+        out["copy_engine"] = copy_rate
     if args.frame_crcs and rank == 0:
         out["frame_crcs"] = timed_crcs
     if work:

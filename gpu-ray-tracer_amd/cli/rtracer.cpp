@@ -194,11 +194,13 @@ int main(int argc, char** argv) {
             if (split) {                                       // every device of the split
                 for (int d = gpus - 1; d >= 0; d--) { (void)hipSetDevice(d); (void)hipDeviceSynchronize(); }
             }
-            else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
-            if (rb) {
+            else if (rb) {
+                // the frames still in flight: each copy as soon as its frame completes, in order,
+                // so the last copies overlap the last frames instead of following all of them
                 while (next_copy < f) copy_frame(true);
                 (void)hipStreamSynchronize(cst);               // every frame is on the host
             }
+            else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
         };
         for (int k = 0; k < 2 * D; k++) issue();          // warm-up: slots, streams, scheduling history
         wait_all();

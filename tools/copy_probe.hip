@@ -1,5 +1,5 @@
 // Probe: which device->pinned-host copy forms run on a copy engine (no CU) on this ROCm.
-// Usage: copy_probe MODE [bytes]; MODE = d2h | default | nocu.
+// Usage: copy_probe MODE [bytes [hipHostMalloc flags]]; MODE = d2h | default | nocu.
 // Prints the mean copy time of 40 copies, then the completion time of one copy issued while a
 // grid that holds every CU spins for 3 ms on another stream: a copy that needs a CU (a blit
 // kernel) finishes after the spin, a copy-engine copy finishes long before it.
@@ -28,7 +28,8 @@ int main(int argc, char** argv) {
                        : !strcmp(mode, "default") ? hipMemcpyDefault : hipMemcpyDeviceToHost;
     void *d, *h; int* dout;
     CK(hipMalloc(&d, n)); CK(hipMalloc(&dout, 4096 * 4));
-    CK(hipHostMalloc(&h, n, hipHostMallocDefault));
+    const unsigned hflags = argc > 3 ? (unsigned)strtoul(argv[3], nullptr, 0) : hipHostMallocDefault;
+    CK(hipHostMalloc(&h, n, hflags));
     std::vector<unsigned> src(n / 4);
     for (size_t i = 0; i < src.size(); i++) src[i] = (unsigned)(i * 2654435761u);
     CK(hipMemcpy(d, src.data(), n, hipMemcpyHostToDevice));
@@ -47,6 +48,33 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%s: %zu B, %.4f ms per copy, %.1f GB/s\n", mode, n, ms / 40, n / (ms / 40 * 1e-3) / 1e9);
+    // the same 40 copies into further fresh host buffers, the first one still held
+    for (int k = 0; k < 3; k++) {
+        void* hk; CK(hipHostMalloc(&hk, n, hflags));
+        for (int w = 0; w < 2; w++) {
+            CK(hipEventRecord(e0, a));
+            for (int i = 0; i < 40; i++) CK(hipMemcpyAsync(hk, d, n, kind, a));
+            CK(hipEventRecord(e1, a));
+            CK(hipStreamSynchronize(a));
+        }
+        float mk = 0;
+        CK(hipEventElapsedTime(&mk, e0, e1));
+        printf("%s: host buffer %d: %.4f ms per copy, %.1f GB/s\n", mode, k + 2, mk / 40, n / (mk / 40 * 1e-3) / 1e9);
+        CK(hipHostFree(hk));
+    }
+    // the same 40 copies on each of 8 fresh streams in turn: a fresh stream may get another engine
+    for (int k = 0; k < 8; k++) {
+        hipStream_t sk; CK(hipStreamCreateWithFlags(&sk, hipStreamNonBlocking));
+        for (int w = 0; w < 2; w++) {
+            CK(hipEventRecord(e0, sk));
+            for (int i = 0; i < 40; i++) CK(hipMemcpyAsync(h, d, n, kind, sk));
+            CK(hipEventRecord(e1, sk));
+            CK(hipStreamSynchronize(sk));
+        }
+        float mk = 0;
+        CK(hipEventElapsedTime(&mk, e0, e1));
+        printf("%s: fresh stream %d: %.4f ms per copy, %.1f GB/s\n", mode, k, mk / 40, n / (mk / 40 * 1e-3) / 1e9);
+    }
     // the same bytes as two halves on two streams at once (two copy engines)
     {
         hipStream_t c2; CK(hipStreamCreateWithFlags(&c2, hipStreamNonBlocking));
