@@ -17,6 +17,7 @@
 // --in-flight D (timing, build extension): --frames frames issued asynchronously with D in
 // flight (rt_scene_set_frame_slots), each into its own device buffer on its own stream, then
 // one wait; prints the time per frame and per slice.  --out then writes the last frame.
+// --overlap sets the frames' grid policy (rt_scene_set_overlap; default stream).
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
@@ -32,7 +33,7 @@ static void usage() {
     std::fprintf(stderr,
                  "usage: rtracer -c CONFIG [-b] [-r] [-s] [-d DIM] [--frames N] [--spp K] [--width W --height H]\n"
                  "               [--out FILE.ppm] [--debug X,Y] [--textures [ATLAS.png]] [--gpus N [--ranks R]]\n"
-                 "               [--in-flight D [--readback]]\n");
+                 "               [--in-flight D [--readback] [--overlap stream|half|full]]\n");
 }
 
 static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
@@ -54,7 +55,7 @@ static bool write_ppm(const char* path, const uint32_t* px, int w, int h) {
 int main(int argc, char** argv) {
     std::string config, out;
     bool bench = false, unopt = false, serial = false, textures = false, readback = false;
-    std::string atlas;
+    std::string atlas, overlap = "stream";
     int dim = 16, frames = 1, spp = 1, width = 0, height = 0, dbg_x = -1, dbg_y = -1, gpus = 1, ranks = 0, in_flight = 0;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
@@ -76,6 +77,10 @@ int main(int argc, char** argv) {
         else if (a == "--ranks") ranks = std::atoi(val("--ranks"));
         else if (a == "--in-flight") in_flight = std::atoi(val("--in-flight"));
         else if (a == "--readback") readback = true;
+        else if (a == "--overlap") {
+            overlap = val("--overlap");
+            if (overlap != "stream" && overlap != "half" && overlap != "full") { usage(); return 2; }
+        }
         else if (a == "--textures") {
             textures = true;
             if (i + 1 < argc && argv[i + 1][0] != '-') atlas = argv[++i];
@@ -126,6 +131,10 @@ int main(int argc, char** argv) {
         const int D = in_flight;
         const bool split = gpus > 1 || ranks > 1;
         rtamd_detail::check(rt_scene_set_frame_slots(handle, D), "rt_scene_set_frame_slots");
+        // the frames are issued back to back: every frame on half the CUs, the first of the
+        // stream included (RT_OVERLAP_STREAM, include/rt_amd.h; bench.py's default --grid)
+        const int policy = overlap == "full" ? RT_OVERLAP_FULL : overlap == "half" ? RT_OVERLAP_HALF : RT_OVERLAP_STREAM;
+        rtamd_detail::check(rt_scene_set_overlap(handle, policy), "rt_scene_set_overlap");
         // --readback (the reference's post-condition for every frame, main.cc's loop blits each
         // canvas): each frame is copied into pinned host memory by a copy engine once it is
         // complete -- the host waits for frame f - (D - 1) as it issues frame f and copies it then,

@@ -194,8 +194,9 @@ int rt_scene_set_frame_slots(rt_scene* s, int n_slots);
  * slots): RT_OVERLAP_HALF (default) = half the CUs, so that two frames' persistent blocks
  * share the GPU and a block's tail (its slowest wave) holds fewer CUs; RT_OVERLAP_FULL =
  * every CU, as a frame issued alone gets.  HALF measured faster for device-resident
- * pipelines (frame -3%, row slices -4..-11%), FULL for pipelines that copy every frame to the
- * host (-12%).  RT_OVERLAP_STREAM = half the CUs for every frame, the
+ * pipelines (frame -3%, row slices -4..-11%); FULL was faster for pipelines whose host copies
+ * ran as blit kernels on the CUs (round 3), not for copy-engine copies (rt_copy_to_host_async,
+ * DESIGN.md §4.2).  RT_OVERLAP_STREAM = half the CUs for every frame, the
  * first of a stream included, for callers that issue frames back to back: the first two
  * frames then run side by side instead of the second waiting for the first's tail (20-frame
  * streams -2%), but a frame issued alone takes half the GPU, so set it for the stream only.
