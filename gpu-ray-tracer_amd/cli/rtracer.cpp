@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -166,17 +167,24 @@ int main(int argc, char** argv) {
             for (auto x : st) ws.push_back(x);
             rtamd_detail::check(rt_copy_engines_warm(ws.data(), (int)ws.size()), "rt_copy_engines_warm");
         }
-        long long f = 0, next_copy = 0;                        // frames [next_copy, f) await their copies
+        long long f = 0;
+        std::deque<long long> uncopied;                        // issued frames whose copies are not yet issued
         const long long lag = D > 1 ? D - 1 : 0;
-        auto copy_frame = [&](bool wait) -> bool {             // the oldest uncopied frame, if complete
-            const int b = (int)(next_copy % NB);
-            if (wait) { if (hipEventSynchronize(ev_done[b]) != hipSuccess) std::exit(1); }
-            else if (hipEventQuery(ev_done[b]) != hipSuccess) return false;
+        // Frames in flight complete out of order (several share the GPU), so a copy is issued as
+        // soon as its own frame is seen complete, not after the older ones: in order only, the
+        // copies trailed their frames by ~4 ms and ~6 of them were left after the last frame
+        // (profiles/r06/cli_window/).  Each frame has its own host buffer.
+        auto copy_frame = [&](long long fr) -> bool {          // frame fr's copy, if the frame is complete
+            const int b = (int)(fr % NB);
+            if (hipEventQuery(ev_done[b]) != hipSuccess) return false;
             rtamd_detail::check(rt_copy_to_host_async(hbuf[b], buf[b], (int64_t)W * H * 4, cst), "rt_copy_to_host_async");
             if (hipEventRecord(ev_copy[b], cst) != hipSuccess) std::exit(1);
             copied[b] = 1;
-            next_copy++;
             return true;
+        };
+        auto copy_done_frames = [&]() {                        // every frame seen complete, oldest first
+            for (auto it = uncopied.begin(); it != uncopied.end();)
+                it = copy_frame(*it) ? uncopied.erase(it) : it + 1;
         };
         auto issue = [&]() {
             const int b = (int)(f % NB);
@@ -192,9 +200,11 @@ int main(int argc, char** argv) {
             rtamd_detail::check(rt_render(handle, &o, nullptr), "rt_render");
             if (rb) {
                 if (hipEventRecord(ev_done[b], st[f % D]) != hipSuccess) std::exit(1);
+                uncopied.push_back(f);
                 f++;
-                while (next_copy < f - lag) copy_frame(true);
-                while (next_copy < f && copy_frame(false)) {}
+                // wait (polling, so younger frames that complete meanwhile are copied too) until
+                // frame f - lag is copied: lag + 1 frames stay in flight
+                do copy_done_frames(); while (!uncopied.empty() && uncopied.front() < f - lag);
                 return;
             }
             f++;
@@ -204,9 +214,9 @@ int main(int argc, char** argv) {
                 for (int d = gpus - 1; d >= 0; d--) { (void)hipSetDevice(d); (void)hipDeviceSynchronize(); }
             }
             else if (rb) {
-                // the frames still in flight: each copy as soon as its frame completes, in order,
-                // so the last copies overlap the last frames instead of following all of them
-                while (next_copy < f) copy_frame(true);
+                // the frames still in flight: each copy as soon as its frame completes, so the
+                // last copies overlap the last frames instead of following all of them
+                while (!uncopied.empty()) copy_done_frames();  // polls: any frame's copy as it completes
                 (void)hipStreamSynchronize(cst);               // every frame is on the host
             }
             else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
