@@ -72,6 +72,57 @@ def test_rows_partition_covers_frame_once():
             assert all(len(rtdist.rows_of(r, g, h)) <= rtdist.slice_height(g, h) for r in range(g))
 
 
+@pytest.mark.parametrize("depth,lag", [(4, 3), (8, 7), (3, 5)])
+def test_frame_pipeline_copies_in_completion_order(depth, lag):
+    """FramePipeline(readback=True) with frames completing out of order (as frames in flight do,
+    several sharing the GPU): a frame's host copy is issued once its own frame is seen complete,
+    before older frames' copies; every frame is copied exactly once, from its own frame buffer
+    before that buffer is rendered again, and the consumer reads frame k - lag as frame k."""
+    import torch
+    import rtamd.dist as rtdist
+    W, H = 8, 4
+    pipe = rtdist.FramePipeline(W, H, 1, 0, "cpu", None, depth=depth, readback=True)
+
+    class Ev:                                   # complete after `delay` completion queries
+        def __init__(self, delay):
+            self.delay = delay
+
+        def synchronize(self):
+            self.delay = 0
+
+    n_ev = [0]
+
+    def event(stream):
+        n_ev[0] += 1
+        return Ev((n_ev[0] * 5) % 7)
+
+    def done(ev):
+        ev.delay -= 1
+        return ev.delay < 0
+    pipe._event, pipe._done = event, done
+    order = []
+    to_host = pipe._to_host
+
+    def logged(k, src, stream):
+        assert int(src[0, 0]) == k              # the buffer still holds frame k when it is copied
+        order.append(k)
+        return to_host(k, src, stream)
+    pipe._to_host = logged
+    n = 4 * depth + 3
+    got = {}
+    for k in range(n):
+        pipe.step(k, lambda buf, st, k=k: buf.fill_(k))
+        if k - lag >= 0:
+            got[k - lag] = pipe.host_frame(k - lag).clone()
+    pipe.finish()
+    for j in range(max(0, n - lag), n):
+        got[j] = pipe.host_frame(j).clone()
+    assert sorted(order) == list(range(n))
+    assert order != sorted(order), "no frame was copied ahead of an older one"
+    for j in range(n):
+        assert torch.equal(got[j], torch.full((H, W), j, dtype=torch.int32)), j
+
+
 def _pipe_main(rank, world, port, scene, w, h, spp, out_path, depth, readback, lag):
     import torch.distributed as dist
     from oracle_lib import Oracle
