@@ -324,6 +324,52 @@ __device__ __forceinline__ void pair_hit_tt2(const float4* rec, const Ray& r, co
         if (active && !k1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
     }
 }
+// pair_hit_tt2 with the lane's activity as its cut ct (active: ct == ct) and the outcome tests
+// issued as four v_cmp into SGPR masks, combined on the scalar unit: the compiler's form of
+// `__ballot(active && !(k0 && k1))` rebuilt the combined mask through a VGPR (v_cndmask 0/1 +
+// v_cmp_ne) before the branch, two VALU and a dependent hand-off per traversal step.
+#ifndef RT_ASM_OUTCOME
+#define RT_ASM_OUTCOME 1
+#endif
+__device__ __forceinline__ void pair_hit_tt2c(const float4* rec, const Ray& r, const RayInv& ri, float ct,
+                                              float& ta, float& tb) {
+#if RT_ASM_OUTCOME
+    const float4 A = rec[0], B = rec[1], C = rec[2];
+    float lo0, hi0, lo1, hi1;
+    slab(r, ri, A.x, A.z, B.x, B.z, C.x, C.z, lo0, hi0);
+    slab(r, ri, A.y, A.w, B.y, B.w, C.y, C.w, lo1, hi1);
+    const float el0 = fmaf(fabsf(lo0), FILT_BOX, FILT_ABS), eh0 = fmaf(fabsf(hi0), FILT_BOX, FILT_ABS);
+    const float el1 = fmaf(fabsf(lo1), FILT_BOX, FILT_ABS), eh1 = fmaf(fabsf(hi1), FILT_BOX, FILT_ABS);
+    const float d0 = lo0 - el0, d1 = lo1 - el1;
+    // certain hit: a <= b; certain miss: c > e (pair_hit_at)
+    const float a0 = fmaxf(lo0 + el0, THRESH), b0 = hi0 - eh0, a1 = fmaxf(lo1 + el1, THRESH), b1 = hi1 - eh1;
+    const float c0 = fmaxf(d0, THRESH), e0 = hi0 + eh0, c1 = fmaxf(d1, THRESH), e1 = hi1 + eh1;
+    const float QNAN = __builtin_nanf("");
+    unsigned long long h0, h1, m0, m1;
+    asm("v_cmp_le_f32 %[h0], %[a0], %[b0]\n\t"
+        "v_cmp_le_f32 %[h1], %[a1], %[b1]\n\t"
+        "v_cmp_gt_f32 %[m0], %[c0], %[e0]\n\t"
+        "v_cmp_gt_f32 %[m1], %[c1], %[e1]\n\t"
+        "v_cndmask_b32 %[ta], %[nan], %[d0], %[h0]\n\t"
+        "v_cndmask_b32 %[tb], %[nan], %[d1], %[h1]\n\t"
+        "s_or_b64 %[m0], %[m0], %[h0]\n\t"                  // outcome of child A certain
+        "s_or_b64 %[m1], %[m1], %[h1]\n\t"                  // ... of child B
+        "s_and_b64 %[m0], %[m0], %[m1]\n\t"
+        "v_cmp_o_f32 %[m1], %[ct], %[ct]\n\t"               // active lanes
+        "s_andn2_b64 %[m0], %[m1], %[m0]"                   // active, some outcome uncertain
+        : [h0] "=&s"(h0), [h1] "=&s"(h1), [m0] "=&s"(m0), [m1] "=&s"(m1), [ta] "=&v"(ta), [tb] "=&v"(tb)
+        : [a0] "v"(a0), [b0] "v"(b0), [a1] "v"(a1), [b1] "v"(b1), [c0] "v"(c0), [e0] "v"(e0), [c1] "v"(c1),
+          [e1] "v"(e1), [d0] "v"(d0), [d1] "v"(d1), [nan] "v"(QNAN), [ct] "v"(ct));
+    if (__builtin_expect(m0 != 0, 0)) {
+        const bool active = ct == ct;
+        const bool k0 = a0 <= b0 || c0 > e0, k1 = a1 <= b1 || c1 > e1;
+        if (active && !k0) ta = box_hit(v3(A.x, A.z, B.x), v3(B.z, C.x, C.z), r) ? -INFINITY : QNAN;
+        if (active && !k1) tb = box_hit(v3(A.y, A.w, B.y), v3(B.w, C.y, C.w), r) ? -INFINITY : QNAN;
+    }
+#else
+    pair_hit_tt2(rec, r, ri, ct == ct, ta, tb);
+#endif
+}
 __device__ __forceinline__ void pair_hit(const float4* np, int k, const Ray& r, const RayInv& ri, bool active,
                                          bool& h0, bool& h1, float& t0, float& t1) {
     pair_hit_at(np + 3 * k, r, ri, active, h0, h1, t0, t1);
@@ -640,7 +686,7 @@ __device__ __forceinline__ bool closest_hit(const SceneView& S, const BvhRefs& b
             const float2 rf = *reinterpret_cast<const float2*>(rec + 3);
             const int ra = uni(__float_as_int(rf.x)), rb = uni(__float_as_int(rf.y));
             float ta, tb;
-            pair_hit_tt2(rec, r, ri, ct == ct, ta, tb);
+            pair_hit_tt2c(rec, r, ri, ct, ta, tb);
             float lt = QNAN, t2 = QNAN;                        // leaf entry bounds (NaN: missed)
             int linst = -1, inst2 = -1, next = -1;             // their instances, the next node (uniform; -1: pop)
             if (bonly) {                                       // popped: leaf B of this node
