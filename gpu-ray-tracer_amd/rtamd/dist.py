@@ -143,7 +143,7 @@ class FramePipeline:
     after its previous gather has completed, its gather buffer after its previous un-permute."""
 
     def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False,
-                 streams=None, host_buffers=None, host_staging=False):
+                 streams=None, host_buffers=None, host_staging=False, copy_lag=None):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
@@ -206,7 +206,11 @@ class FramePipeline:
             # copies trail the frames issued by `lag`: the host waits for frame k - lag as it issues
             # frame k, so lag + 1 frames stay in flight (one rank: depth, as device-resident frames;
             # N > 1: depth - 1, the un-permute targets are reused after depth frames)
+            # (copy_lag: a longer wait before the host blocks, within the buffers: one rank up to
+            # 2 depth - 2, N > 1 up to depth - 2)
             self.lag = max(0, D - 1) if world == 1 else max(0, D - 2)
+            if copy_lag is not None:
+                self.lag = max(0, min(int(copy_lag), self.n_parts - 2 if world == 1 else D - 2))
             self.deferred = []                      # (frame, source, ready event, ("part" | "out", slot))
             if self.cuda:
                 # The runtime gives a copy issued while an earlier one still runs the next idle SDMA
