@@ -84,6 +84,9 @@ def parse():
                    help="no per-frame HIP events (then trace_kernel_ms / roofline are not measured)")
     p.add_argument("--no-overlap", action="store_true", help="serial frames (no frame pipeline)")
     p.add_argument("--frames-in-flight", type=int, default=8, help="frame pipeline depth (1-8)")
+    p.add_argument("--copy-streams", type=int, default=2,
+                   help="host-readable pipeline: copy streams the frames' copies alternate over "
+                        "(rtamd.dist.FramePipeline copy_streams; DESIGN.md 4.2)")
     p.add_argument("--copy-lag", type=int, default=None,
                    help="host-readable pipeline: the host waits for frame k - L's copy as it issues frame k "
                         "(default depth - 1; rtamd.dist.FramePipeline copy_lag)")
@@ -269,10 +272,10 @@ def main():
         # first used here, before the scene exists: a torch stream's HIP stream is created at its
         # first use (1-7 ms each, profiles/r06/cold/), the caller's one-time cost, not a frame's.
         fbr = rtdist.FramePipeline(W0, H0, world, rank, "cuda", dist, depth=depth, readback=True, host_staging=gloo,
-                                   copy_lag=args.copy_lag)
+                                   copy_lag=args.copy_lag, copy_streams=args.copy_streams)
         fb = rtdist.FramePipeline(W0, H0, world, rank, "cuda", dist, depth=depth, streams=fbr.streams,
                                   host_staging=gloo)
-        for st_ in fbr.streams + ([fbr.copy_stream] if getattr(fbr, "copy_stream", None) is not None else []):
+        for st_ in fbr.streams + [c for c in getattr(fbr, "copy_streams", []) if c is not None]:
             torch.cuda.Event().record(st_)
         torch.cuda.synchronize()
     scene_path = os.path.join(ROOT, "scenes", args.scene + ".json")

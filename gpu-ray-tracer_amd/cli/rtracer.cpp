@@ -20,6 +20,7 @@
 // --overlap sets the frames' grid policy (rt_scene_set_overlap; default stream).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -148,7 +149,11 @@ int main(int argc, char** argv) {
         std::vector<uint32_t*> hbuf(rb ? NB : 0);
         std::vector<hipEvent_t> ev_done(NB), ev_copy(NB);
         std::vector<char> copied(NB, 0);
-        hipStream_t cst = nullptr;
+        // the frames' copies alternate over two copy streams (RT_CLI_COPY_STREAMS: 1-4): on one
+        // copy-engine queue consecutive copies left ~85-us gaps and a growing backlog
+        // (profiles/r06/cli_api/); two queues: world8 +4-12% -> +0.3-2% (profiles/r06/cli_cs/)
+        const int ncs = !rb ? 1 : getenv("RT_CLI_COPY_STREAMS") ? std::max(1, std::min(4, atoi(getenv("RT_CLI_COPY_STREAMS")))) : 2;
+        std::vector<hipStream_t> csts(ncs, nullptr);
         for (int k = 0; k < D; k++)
             if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); return 1; }
         for (int k = 0; k < NB; k++) {
@@ -162,8 +167,9 @@ int main(int argc, char** argv) {
             }
         }
         if (rb) {
-            if (hipStreamCreateWithFlags(&cst, hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); return 1; }
-            std::vector<void*> ws{cst};
+            for (auto& c : csts)
+                if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) { std::fprintf(stderr, "HIP stream failed\n"); return 1; }
+            std::vector<void*> ws(csts.begin(), csts.end());
             for (auto x : st) ws.push_back(x);
             rtamd_detail::check(rt_copy_engines_warm(ws.data(), (int)ws.size()), "rt_copy_engines_warm");
         }
@@ -177,8 +183,9 @@ int main(int argc, char** argv) {
         auto copy_frame = [&](long long fr) -> bool {          // frame fr's copy, if the frame is complete
             const int b = (int)(fr % NB);
             if (hipEventQuery(ev_done[b]) != hipSuccess) return false;
-            rtamd_detail::check(rt_copy_to_host_async(hbuf[b], buf[b], (int64_t)W * H * 4, cst), "rt_copy_to_host_async");
-            if (hipEventRecord(ev_copy[b], cst) != hipSuccess) std::exit(1);
+            hipStream_t c = csts[fr % ncs];
+            rtamd_detail::check(rt_copy_to_host_async(hbuf[b], buf[b], (int64_t)W * H * 4, c), "rt_copy_to_host_async");
+            if (hipEventRecord(ev_copy[b], c) != hipSuccess) std::exit(1);
             copied[b] = 1;
             return true;
         };
@@ -217,7 +224,7 @@ int main(int argc, char** argv) {
                 // the frames still in flight: each copy as soon as its frame completes, so the
                 // last copies overlap the last frames instead of following all of them
                 while (!uncopied.empty()) copy_done_frames();  // polls: any frame's copy as it completes
-                (void)hipStreamSynchronize(cst);               // every frame is on the host
+                for (auto c : csts) (void)hipStreamSynchronize(c);   // every frame is on the host
             }
             else for (int k = 0; k < D; k++) (void)hipStreamSynchronize(st[k]);
         };
@@ -246,7 +253,7 @@ int main(int argc, char** argv) {
             (void)hipFree(buf[k]);
             if (rb) { (void)rt_host_free(hbuf[k]); (void)hipEventDestroy(ev_done[k]); (void)hipEventDestroy(ev_copy[k]); }
         }
-        if (cst) (void)hipStreamDestroy(cst);
+        for (auto c : csts) if (c) (void)hipStreamDestroy(c);
         renv::gpu::Scene::free(*scene);
         delete scene;
         return 0;

@@ -143,7 +143,7 @@ class FramePipeline:
     after its previous gather has completed, its gather buffer after its previous un-permute."""
 
     def __init__(self, width, height, world, rank, device, dist=None, dtype=torch.int32, depth=2, readback=False,
-                 streams=None, host_buffers=None, host_staging=False, copy_lag=None):
+                 streams=None, host_buffers=None, host_staging=False, copy_lag=None, copy_streams=2):
         self.W, self.H, self.world, self.rank, self.dist = width, height, world, rank, dist
         self.depth = D = max(1, int(depth))
         self.rows = slice_height(world, height)
@@ -201,7 +201,14 @@ class FramePipeline:
             # measured 0.5-5.6 ms from frame done to copy done for a 0.16-ms copy, a convoy that
             # held the frames behind it (0.68 ms per frame against 0.59 device-resident); with
             # the copies issued on completion 0.59-0.61 (profiles/r06/rbprobe/).
-            self.copy_stream = torch.cuda.Stream(device=device) if self.cuda else None
+            # Frames' copies alternate over `copy_streams` copy streams (the runtime puts each on its
+            # own copy-engine queue): consecutive copies on one queue left gaps of ~85 us between
+            # them and a backlog of ~10 copies behind the frames under a trace (enqueue -> start
+            # 3.1 ms median); two queues overlap those gaps (CLI, 100 frames, world8: +4-12% ->
+            # +0.3-2% over device-resident; profiles/r06/cli_cs/, profiles/r06/cli_api/).
+            self.copy_streams = ([torch.cuda.Stream(device=device) for _ in range(max(1, int(copy_streams)))]
+                                 if self.cuda else [None])
+            self.copy_stream = self.copy_streams[0]
             self.copy_done = [None] * self.n_parts  # one rank: the copy that last read parts[p]
             # copies trail the frames issued by `lag`: the host waits for frame k - lag as it issues
             # frame k, so lag + 1 frames stay in flight (one rank: depth, as device-resident frames;
@@ -217,7 +224,7 @@ class FramePipeline:
                 # engine, and a copy's first use of an engine creates its queue (~7 ms inside the
                 # enqueue, profiles/r06/rblog/): start the engines these streams will use now.
                 from . import copy_engines_warm
-                copy_engines_warm([self.copy_stream.cuda_stream] + [st.cuda_stream for st in self.streams])
+                copy_engines_warm([c.cuda_stream for c in self.copy_streams] + [st.cuda_stream for st in self.streams])
         self.work = [None] * D          # gather of the frame last rendered in each slot
         self.unperm = [None] * D        # event after the un-permute that last read each gather buffer
         self.pending = [False] * D      # slot's frame gathered but not yet un-permuted
@@ -261,7 +268,7 @@ class FramePipeline:
     def _copy_deferred(self, i):
         """Issue deferred host copy i (its frame has completed)."""
         k, src, ev, (kind, s) = self.deferred.pop(i)
-        done = self._to_host(k, src, self.copy_stream)
+        done = self._to_host(k, src, self.copy_streams[k % len(self.copy_streams)])
         if kind == "part":
             self.copy_done[s] = done
         else:
